@@ -1,0 +1,160 @@
+/*
+ * ptamd.h — C ABI of the MI355X-native path tracer (libptamd.so).
+ *
+ * Drop-in boundary for the render path of Damo12320/OptixPathtracer.  Each entry point
+ * names the reference interface it replaces (paths relative to
+ * OptixPathtracer/source/).  Plain C types only: pointers, sizes, int status codes.
+ * Status: 0 = ok, < 0 = error (message via pt_last_error()).  Host pointers unless an
+ * argument is documented as a device pointer.  Colour buffers are W*H*3 fp32, RGB
+ * interleaved (glm::vec3 AoS as Renderer/OptiX/LaunchParams.h:12), row 0 = bottom
+ * (OpenGL convention of devicePrograms.cu:607-608,704).
+ */
+#ifndef PTAMD_H
+#define PTAMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_ERR_INVALID (-1)
+#define PT_ERR_HIP (-2)
+#define PT_ERR_STATE (-3)
+#define PT_ERR_NOMEM (-4)
+
+/* Material mode = which BSDF pair the closest-hit program uses.  The reference selects it
+ * by (un)commenting lines in Renderer/OptiX/devicePrograms.cu:303-341. */
+#define PT_MAT_DEFAULT 0    /* rnd < metallic ? Conductor : GlossyDiffuse (active reference code) */
+#define PT_MAT_LAMBERT 1    /* devicePrograms.cu:306 / :326 */
+#define PT_MAT_CONDUCTOR 2  /* devicePrograms.cu:307 / :327 */
+#define PT_MAT_DIELECTRIC 3 /* devicePrograms.cu:304 / :324 */
+#define PT_MAT_LAYERED 4    /* devicePrograms.cu:305 / :325 */
+
+/* Render-kernel variants (all produce the same image). */
+#define PT_KERNEL_MEGA 0      /* one thread per pixel, frames looped in registers */
+#define PT_KERNEL_WAVEFRONT 1 /* persistent wavefront: SoA ray/hit queues, wave compaction */
+
+/* Mesh: ModelLoading/Mesh.h:9-45 (vertecies, normal, texCoord, index, ModelMatrix, albedo,
+ * metallic, roughness, texture ids).  Borrowed only during pt_create (deep copy). */
+typedef struct pt_mesh {
+    const float* vertices;    /* n_vertices * 3 */
+    const float* normals;     /* n_vertices * 3, or NULL (reference then yields NaN shading normals) */
+    const float* texcoords;   /* n_vertices * 2, or NULL */
+    const int32_t* indices;   /* n_triangles * 3 (glm::ivec3 index, Mesh.h:20) */
+    int32_t n_vertices;
+    int32_t n_triangles;
+    float model_matrix[16];   /* column-major glm::mat4 = Mesh::GetModelMatrix() (Mesh.cpp:6-22) */
+    float albedo[3];
+    float metallic;
+    float roughness;
+    int32_t albedo_tex;       /* -1 = none (Mesh.h:35-37) */
+    int32_t normal_tex;
+    int32_t metal_rough_tex;
+} pt_mesh;
+
+/* Texture: ModelLoading/Texture.h:5-12 (RGBA8 pixels). */
+typedef struct pt_texture {
+    const uint32_t* rgba8;
+    int32_t width;
+    int32_t height;
+} pt_texture;
+
+/* Model: ModelLoading/Model.h:5-8. */
+typedef struct pt_scene {
+    const pt_mesh* meshes;
+    int32_t n_meshes;
+    const pt_texture* textures;
+    int32_t n_textures;
+} pt_scene;
+
+/* PointLight: Renderer/OptiX/LightsStruct.h:6-10. */
+typedef struct pt_point_light {
+    float position[3];
+    float color[3];
+} pt_point_light;
+
+typedef struct pt_options {
+    int32_t device;         /* HIP device ordinal (reference hard-codes device 0, OptixRenderer.cpp:70) */
+    int32_t material_mode;  /* PT_MAT_* */
+    int32_t kernel;         /* PT_KERNEL_* */
+    int32_t reserved[5];
+} pt_options;
+
+typedef struct pt_stats {
+    uint64_t segments;        /* radiance rays traced (path segments) since pt_stats_reset */
+    uint64_t samples;         /* camera paths since pt_stats_reset */
+    double last_render_ms;    /* device time of the last render call (HIP events, library stream) */
+    double total_render_ms;   /* summed device time since pt_stats_reset */
+    uint64_t render_calls;
+    double bvh_build_ms;      /* LBVH build device time (pt_create) */
+    int32_t bvh_nodes;        /* internal nodes */
+    int32_t triangles;
+} pt_stats;
+
+typedef struct pt_renderer pt_renderer;
+
+/* OptixRenderer::OptixRenderer(ptxPath, Model*) — Renderer/OptiX/OptixRenderer.cpp:9-36.
+ * Uploads the scene and builds the LBVH on the GPU (replaces BuildAccel, :306-456). */
+int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** out);
+/* no destructor in the reference (it leaks); frees every device buffer. */
+int pt_destroy(pt_renderer* r);
+
+/* OptixRenderer::Resize(glm::ivec2&) — OptixRenderer.cpp:649-660.  0-sized = no-op. */
+int pt_resize(pt_renderer* r, int32_t width, int32_t height);
+/* OptixRenderer::SetCamera(Camera*) — OptixRenderer.cpp:662-668: position + inverse view +
+ * inverse projection, column-major glm::mat4. */
+int pt_set_camera(pt_renderer* r, const float position[3], const float inverse_view[16],
+                  const float inverse_projection[16]);
+/* OptixRenderer::SetLights(std::vector<PointLight>*) — OptixRenderer.cpp:670-675 (re-settable). */
+int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count);
+/* OptixRenderer::SetMaxBounces(int) — OptixRenderer.cpp:677-679. */
+int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces);
+int pt_set_material_mode(pt_renderer* r, int32_t material_mode);
+int pt_set_kernel(pt_renderer* r, int32_t kernel);
+
+/* OptixRenderer::Render(glm::vec3 h_pixels[]) — OptixRenderer.cpp:617-647: frame.id++,
+ * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before
+ * the first pt_resize (as :621). */
+int pt_render(pt_renderer* r, float* host_rgb);
+
+/* Device-resident accumulation (replaces the per-spp download + GL blend of
+ * Renderer/OptixView.cpp:201-255 / AddPathtracedFrame.frag:18-24).  Renders frame ids
+ * first_frame_id .. first_frame_id+n_frames-1 and ADDS each sample's radiance, in frame
+ * order, into the fp32 sum buffer.  Asynchronous on the library stream. */
+int pt_accum_clear(pt_renderer* r);
+int pt_render_frames(pt_renderer* r, uint32_t first_frame_id, uint32_t n_frames);
+/* Use caller-owned device memory (W*H*3 floats) as the sum buffer (e.g. an RCCL buffer);
+ * NULL reverts to the internal buffer. */
+int pt_set_accum_device_buffer(pt_renderer* r, float* device_sum_rgb);
+float* pt_accum_device_ptr(pt_renderer* r);
+/* Download the sum (scale = 1) or the mean (scale = 1/spp) to host. */
+int pt_accum_download(pt_renderer* r, float* host_rgb, float scale);
+
+int pt_synchronize(pt_renderer* r);
+void* pt_stream(pt_renderer* r);   /* hipStream_t of the library */
+uint32_t pt_frame_id(const pt_renderer* r);
+int pt_set_frame_id(pt_renderer* r, uint32_t frame_id);
+int pt_get_stats(pt_renderer* r, pt_stats* out);
+int pt_stats_reset(pt_renderer* r);
+
+/* Camera helper: Renderer/Camera.cpp:6-70 + GlmHelperMethods.cpp:4-10 (Blender position /
+ * rotation in degrees -> engine position, inverse view, inverse projection for the given
+ * frame size; "horizontal" FOV used as fovy, as the reference does). */
+int pt_camera_from_blender(const float blender_position[3], const float blender_rotation_deg[3],
+                           float fov_deg, int32_t width, int32_t height, float position[3],
+                           float inverse_view[16], float inverse_projection[16]);
+
+/* Debug / parity: trace n rays (origin xyz, dir xyz, tmin, tmax per ray = 8 floats) against
+ * the LBVH.  prim = global triangle index (meshes concatenated) or -1. */
+int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* prim, float* t,
+                  float* u, float* v, int32_t* backface, int32_t any_hit);
+
+const char* pt_last_error(void);
+const char* pt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTAMD_H */

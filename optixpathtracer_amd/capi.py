@@ -1,0 +1,156 @@
+"""ctypes binding of libptamd.so — the C ABI declared in include/ptamd.h.
+
+The shared library is built in-tree (``optixpathtracer_amd/libptamd.so``, see
+``__graft_entry__.build``).  There is no fallback: if the library is missing or a call
+fails, a :class:`PTError` is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libptamd.so"
+
+PT_MAT_DEFAULT, PT_MAT_LAMBERT, PT_MAT_CONDUCTOR, PT_MAT_DIELECTRIC, PT_MAT_LAYERED = range(5)
+PT_KERNEL_MEGA, PT_KERNEL_WAVEFRONT = 0, 1
+
+MATERIAL_MODES = {
+    "default": PT_MAT_DEFAULT,
+    "lambert": PT_MAT_LAMBERT,
+    "conductor": PT_MAT_CONDUCTOR,
+    "dielectric": PT_MAT_DIELECTRIC,
+    "layered": PT_MAT_LAYERED,
+}
+
+
+class PTError(RuntimeError):
+    """A libptamd call returned a negative status."""
+
+
+class pt_mesh(C.Structure):
+    _fields_ = [
+        ("vertices", C.POINTER(C.c_float)),
+        ("normals", C.POINTER(C.c_float)),
+        ("texcoords", C.POINTER(C.c_float)),
+        ("indices", C.POINTER(C.c_int32)),
+        ("n_vertices", C.c_int32),
+        ("n_triangles", C.c_int32),
+        ("model_matrix", C.c_float * 16),
+        ("albedo", C.c_float * 3),
+        ("metallic", C.c_float),
+        ("roughness", C.c_float),
+        ("albedo_tex", C.c_int32),
+        ("normal_tex", C.c_int32),
+        ("metal_rough_tex", C.c_int32),
+    ]
+
+
+class pt_texture(C.Structure):
+    _fields_ = [("rgba8", C.POINTER(C.c_uint32)), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class pt_scene(C.Structure):
+    _fields_ = [
+        ("meshes", C.POINTER(pt_mesh)),
+        ("n_meshes", C.c_int32),
+        ("textures", C.POINTER(pt_texture)),
+        ("n_textures", C.c_int32),
+    ]
+
+
+class pt_point_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("color", C.c_float * 3)]
+
+
+class pt_options(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("material_mode", C.c_int32),
+        ("kernel", C.c_int32),
+        ("reserved", C.c_int32 * 5),
+    ]
+
+
+class pt_stats(C.Structure):
+    _fields_ = [
+        ("segments", C.c_uint64),
+        ("samples", C.c_uint64),
+        ("last_render_ms", C.c_double),
+        ("total_render_ms", C.c_double),
+        ("render_calls", C.c_uint64),
+        ("bvh_build_ms", C.c_double),
+        ("bvh_nodes", C.c_int32),
+        ("triangles", C.c_int32),
+    ]
+
+
+_FP = C.POINTER(C.c_float)
+_IP = C.POINTER(C.c_int32)
+_R = C.c_void_p  # pt_renderer*
+
+# name -> (restype, argtypes); this is the complete exported surface of include/ptamd.h
+SIGNATURES = {
+    "pt_create": (C.c_int, [C.POINTER(pt_scene), C.POINTER(pt_options), C.POINTER(C.c_void_p)]),
+    "pt_destroy": (C.c_int, [_R]),
+    "pt_resize": (C.c_int, [_R, C.c_int32, C.c_int32]),
+    "pt_set_camera": (C.c_int, [_R, _FP, _FP, _FP]),
+    "pt_set_lights": (C.c_int, [_R, C.POINTER(pt_point_light), C.c_int32]),
+    "pt_set_max_bounces": (C.c_int, [_R, C.c_int32]),
+    "pt_set_material_mode": (C.c_int, [_R, C.c_int32]),
+    "pt_set_kernel": (C.c_int, [_R, C.c_int32]),
+    "pt_render": (C.c_int, [_R, _FP]),
+    "pt_accum_clear": (C.c_int, [_R]),
+    "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),
+    "pt_set_accum_device_buffer": (C.c_int, [_R, C.c_void_p]),
+    "pt_accum_device_ptr": (C.c_void_p, [_R]),
+    "pt_accum_download": (C.c_int, [_R, _FP, C.c_float]),
+    "pt_synchronize": (C.c_int, [_R]),
+    "pt_stream": (C.c_void_p, [_R]),
+    "pt_frame_id": (C.c_uint32, [_R]),
+    "pt_set_frame_id": (C.c_int, [_R, C.c_uint32]),
+    "pt_get_stats": (C.c_int, [_R, C.POINTER(pt_stats)]),
+    "pt_stats_reset": (C.c_int, [_R]),
+    "pt_camera_from_blender": (C.c_int, [_FP, _FP, C.c_float, C.c_int32, C.c_int32, _FP, _FP, _FP]),
+    "pt_trace_rays": (C.c_int, [_R, _FP, C.c_int32, _IP, _FP, _FP, _FP, _IP, C.c_int32]),
+    "pt_last_error": (C.c_char_p, []),
+    "pt_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path: str | os.PathLike | None = None) -> C.CDLL:
+    """Load libptamd.so (in-tree).  Raises PTError if it has not been built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise PTError(
+            f"{p} not found: the HIP extension is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)"
+        )
+    lib = C.CDLL(str(p))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = load().pt_last_error()
+        raise PTError(f"{what} failed ({status}): {msg.decode() if msg else ''}")
+
+
+def fptr(a):
+    """float32 contiguous numpy array -> float*"""
+    return a.ctypes.data_as(_FP)
+
+
+def iptr(a):
+    return a.ctypes.data_as(_IP)

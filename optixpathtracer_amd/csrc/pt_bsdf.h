@@ -1,0 +1,589 @@
+// pt_bsdf.h — the reference's BSDF models as gfx950 device code.
+//
+// Behaviour follows Renderer/OptiX/PBRT/{Microfacet,Conductor,LambertDiffuse,Dielectric,
+// GlossyDiffuse}.h of Damo12320/OptixPathtracer (line numbers cited per function).  All
+// evaluation happens in the shading frame (N = +z).  RNG draws consume the path seed in the
+// reference order (SURVEY.md §8(a) "RNG draw order"); the Layered walk's Russian-roulette
+// draws use the private TEA stream the reference derives from wo/wi.
+#pragma once
+#include "pt_math.h"
+
+namespace pt {
+
+constexpr float kInvPi = 0.31830988618379067154f;
+
+struct BSample {
+    f3 color;
+    float pdf;
+    f3 dir;
+    bool refl, trans, spec;
+};
+
+// ---- sampling primitives ----------------------------------------------------------------
+// random.h:76-84 (u0 then u1, left-to-right as in devicePrograms.cu.ptx)
+__device__ __forceinline__ void disk_polar(uint32_t& seed, float& px, float& py) {
+    const float pi = (float)3.14159265359;
+    float u0 = rnd(seed);
+    float u1 = rnd(seed);
+    float r = sqrtf(u0);
+    float theta = 2.0f * pi * u1;
+    px = r * cosf(theta);
+    py = r * sinf(theta);
+}
+// LambertDiffuse.h:35-55
+__device__ __forceinline__ void disk_concentric(uint32_t& seed, float& dx, float& dy) {
+    const float PiOver4 = 0.78539816339744830961f;
+    const float PiOver2 = 1.57079632679489661923f;
+    float u0 = rnd(seed);
+    float u1 = rnd(seed);
+    float ox = 2.0f * u0 - 1.0f, oy = 2.0f * u1 - 1.0f;
+    if (ox == 0.0f && oy == 0.0f) {
+        dx = 0.0f;
+        dy = 0.0f;
+        return;
+    }
+    float theta, r;
+    if (gabs(ox) > gabs(oy)) {
+        r = ox;
+        theta = PiOver4 * (oy / ox);
+    } else {
+        r = oy;
+        theta = PiOver2 - PiOver4 * (ox / oy);
+    }
+    dx = r * cosf(theta);
+    dy = r * sinf(theta);
+}
+
+// ---- spherical geometry: SphericalGeometry.h:8-29 ----------------------------------------
+__device__ __forceinline__ float cos2_theta(f3 w) { return sqr(w.z); }
+__device__ __forceinline__ float abs_cos_theta(f3 w) { return gabs(w.z); }
+__device__ __forceinline__ float sin2_theta(f3 w) { return gmax(0.0f, 1.0f - cos2_theta(w)); }
+__device__ __forceinline__ float sin_theta(f3 w) { return sqrtf(sin2_theta(w)); }
+__device__ __forceinline__ float tan2_theta(f3 w) { return sin2_theta(w) / cos2_theta(w); }
+__device__ __forceinline__ float cos_phi(f3 w) {
+    float s = sin_theta(w);
+    return (s == 0.0f) ? 1.0f : gclamp(w.x / s, -1.0f, 1.0f);
+}
+__device__ __forceinline__ float sin_phi(f3 w) {
+    float s = sin_theta(w);
+    return (s == 0.0f) ? 0.0f : gclamp(w.y / s, -1.0f, 1.0f);
+}
+__device__ __forceinline__ bool same_hemisphere(f3 w, f3 wp) { return w.z * wp.z > 0.0f; }
+
+// ---- Trowbridge-Reitz: Microfacet.h:9-119 ------------------------------------------------
+__device__ __forceinline__ float tr_D(f3 wm, float alpha) {
+    const float pi = 3.14159265359f;
+    float t2 = tan2_theta(wm);
+    if (isinf(t2)) return 0.0f;
+    float cos4 = sqr(cos2_theta(wm));
+    if (cos4 < 1e-16f) return 0.0f;
+    float e = t2 * (sqr(cos_phi(wm) / alpha) + sqr(sin_phi(wm) / alpha));
+    return 1.0f / (pi * alpha * alpha * cos4 * sqr(1.0f + e));
+}
+__device__ __forceinline__ float tr_lambda(f3 w, float alpha) {
+    float t2 = tan2_theta(w);
+    if (isinf(t2)) return 0.0f;
+    float a2 = sqr(cos_phi(w) * alpha) + sqr(sin_phi(w) * alpha);
+    return (sqrtf(1.0f + a2 * t2) - 1.0f) / 2.0f;
+}
+__device__ __forceinline__ float tr_G(f3 wo, f3 wi, float alpha) {
+    return 1.0f / (1.0f + tr_lambda(wo, alpha) + tr_lambda(wi, alpha));
+}
+__device__ __forceinline__ float tr_G1(f3 w, float alpha) { return 1.0f / (1.0f + tr_lambda(w, alpha)); }
+__device__ __forceinline__ float tr_pdf(f3 w, f3 wm, float alpha) {   // D(w, wm): :81-88
+    return tr_G1(w, alpha) / abs_cos_theta(w) * tr_D(wm, alpha) * abs_dot(w, wm);
+}
+__device__ __forceinline__ f3 tr_sample_wm(uint32_t& seed, f3 w, float alpha) {  // :90-119
+    f3 wh = normalize(mk(alpha * w.x, alpha * w.y, w.z));
+    if (wh.z < 0.0f) wh = -wh;
+    f3 T1 = (wh.z < 0.99999f) ? normalize(cross(mk(0.0f, 0.0f, 1.0f), wh)) : mk(1.0f, 0.0f, 0.0f);
+    f3 T2 = cross(wh, T1);
+    float px, py;
+    disk_polar(seed, px, py);
+    float h = sqrtf(1.0f - sqr(px));
+    float x = (1.0f + wh.z) / 2.0f;
+    py = (1.0f - x) * h + x * py;
+    float pz = sqrtf(gmax(0.0f, 1.0f - (sqr(px) + sqr(py))));
+    f3 nh = mk(px * T1.x + py * T2.x + pz * wh.x, px * T1.y + py * T2.y + pz * wh.y,
+               px * T1.z + py * T2.z + pz * wh.z);
+    return normalize(mk(alpha * nh.x, alpha * nh.y, gmax(1e-6f, nh.z)));
+}
+
+// ---- Conductor: Conductor.h:42-190, Complex.h:5-63 ---------------------------------------
+struct cpx {
+    float re, im;
+};
+__device__ __forceinline__ cpx c_add(cpx a, cpx b) { return cpx{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cpx c_sub(cpx a, cpx b) { return cpx{a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cpx c_mul(cpx a, cpx b) {
+    return cpx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__device__ __forceinline__ cpx c_div(cpx a, cpx z) {
+    float scale = 1.0f / (z.re * z.re + z.im * z.im);
+    return cpx{scale * (a.re * z.re + a.im * z.im), scale * (a.im * z.re - a.re * z.im)};
+}
+__device__ __forceinline__ float c_norm(cpx z) { return z.re * z.re + z.im * z.im; }
+__device__ __forceinline__ cpx c_sqrt(cpx z) {
+    float n = sqrtf(c_norm(z));
+    float t1 = sqrtf(0.5f * (n + gabs(z.re)));
+    float t2 = 0.5f * z.im / t1;
+    if (n == 0.0f) return cpx{0.0f, 0.0f};
+    if (z.re >= 0.0f) return cpx{t1, t2};
+    return cpx{gabs(t2), copysignf(t1, z.im)};
+}
+__device__ __forceinline__ float fr_complex(float cos_i, cpx eta) {  // :42-52
+    cos_i = gclamp(cos_i, 0.0f, 1.0f);
+    float sin2i = 1.0f - sqr(cos_i);
+    cpx sin2t = c_div(cpx{sin2i, 0.0f}, c_mul(eta, eta));
+    cpx cost = c_sqrt(c_sub(cpx{1.0f, 0.0f}, sin2t));
+    cpx ec = c_mul(eta, cpx{cos_i, 0.0f});
+    cpx r_parl = c_div(c_sub(ec, cost), c_add(ec, cost));
+    cpx ect = c_mul(eta, cost);
+    cpx r_perp = c_div(c_sub(cpx{cos_i, 0.0f}, ect), c_add(cpx{cos_i, 0.0f}, ect));
+    return (c_norm(r_parl) + c_norm(r_perp)) / 2.0f;
+}
+__device__ __forceinline__ float fresnel_complex1(float cos_i, float refl) {  // :54-92, one channel
+    float r = gclamp(refl, 0.0f, 0.9999f);
+    float om = 1.0f - r;
+    om = om > 0.0f ? om : 0.0f;
+    float k = 2.0f * sqrtf(r) / sqrtf(om);
+    return fr_complex(cos_i, cpx{1.0f, k});
+}
+__device__ __forceinline__ f3 fresnel_complex(float cos_i, f3 refl) {
+    return mk(fresnel_complex1(cos_i, refl.x), fresnel_complex1(cos_i, refl.y),
+              fresnel_complex1(cos_i, refl.z));
+}
+__device__ __forceinline__ f3 conductor_f(f3 albedo, float roughness, f3 wo, f3 wi) {  // :97-120
+    float alpha = sqr(roughness);
+    if (!same_hemisphere(wo, wi)) return mk(0, 0, 0);
+    if (alpha < 1e-3f) return mk(0, 0, 0);
+    float co = abs_cos_theta(wo), ci = abs_cos_theta(wi);
+    if (ci == 0.0f || co == 0.0f) return mk(0, 0, 0);
+    f3 wm = wi + wo;
+    if (length_sqr(wm) == 0.0f) return mk(0, 0, 0);
+    wm = normalize(wm);
+    f3 F = fresnel_complex(abs_dot(wo, wm), albedo);
+    float D = tr_D(wm, alpha), G = tr_G(wo, wi, alpha);
+    float den = 4.0f * ci * co;
+    return mk(D * F.x * G / den, D * F.y * G / den, D * F.z * G / den);
+}
+__device__ __forceinline__ bool conductor_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo,
+                                                 BSample& s) {  // :122-190
+    float alpha = sqr(roughness);
+    if (alpha < 1e-3f) {
+        f3 wi = mk(-wo.x, -wo.y, wo.z);
+        float ac = abs_cos_theta(wi);
+        s.color = fresnel_complex(ac, albedo) / ac;
+        s.dir = wi;
+        s.pdf = 1.0f;
+        s.refl = true;
+        s.trans = false;
+        s.spec = true;
+        return true;
+    }
+    if (wo.z == 0.0f) return false;
+    f3 wm = tr_sample_wm(seed, wo, alpha);
+    float d2 = 2.0f * dot(wo, wm);
+    f3 wi = (-wo) + d2 * wm;
+    if (!same_hemisphere(wo, wi)) return false;
+    float pdf = tr_pdf(wo, wm, alpha) / (4.0f * abs_dot(wo, wm));
+    float co = abs_cos_theta(wo), ci = abs_cos_theta(wi);
+    if (ci == 0.0f || co == 0.0f) return false;
+    f3 F = fresnel_complex(abs_dot(wo, wm), albedo);
+    float D = tr_D(wm, alpha), G = tr_G(wo, wi, alpha);
+    float den = 4.0f * ci * co;
+    s.color = mk(D * F.x * G / den, D * F.y * G / den, D * F.z * G / den);
+    s.dir = wi;
+    s.pdf = pdf;
+    s.refl = true;
+    s.trans = false;
+    s.spec = false;
+    return true;
+}
+
+// ---- Lambert: LambertDiffuse.h:86-140 ------------------------------------------------------
+__device__ __forceinline__ f3 lambert_f(f3 albedo, f3 wo, f3 wi) {
+    if (!same_hemisphere(wo, wi)) return mk(0, 0, 0);
+    return albedo * kInvPi;
+}
+// z forced >= 0 whatever wo's hemisphere (:115-119)
+__device__ __forceinline__ bool lambert_sample(uint32_t& seed, f3 albedo, bool reflection, BSample& s) {
+    if (!reflection) return false;
+    float dx, dy;
+    disk_concentric(seed, dx, dy);
+    float z = sqrtf(gmax(0.0f, 1.0f - sqr(dx) - sqr(dy)));
+    f3 d = mk(dx, dy, z);
+    if (d.z < 0.0f) d.z *= -1.0f;
+    d = normalize(d);
+    s.dir = d;
+    s.pdf = abs_cos_theta(d) * kInvPi;
+    s.color = albedo * kInvPi;
+    s.refl = true;
+    s.trans = false;
+    s.spec = false;
+    return true;
+}
+__device__ __forceinline__ float lambert_pdf(f3 wo, f3 wi, bool reflection) {
+    if (!reflection || !same_hemisphere(wi, wo)) return 0.0f;
+    return abs_cos_theta(wi) * kInvPi;
+}
+
+// ---- Dielectric (eta = 1.5): Dielectric.h:20-343 -------------------------------------------
+enum { kRadiance = 0, kImportance = 1 };
+__device__ __forceinline__ float fresnel_dielectric(float cos_i, float ior) {  // :20-42
+    cos_i = gclamp(cos_i, -1.0f, 1.0f);
+    if (cos_i < 0.0f) {
+        ior = 1.0f / ior;
+        cos_i = -cos_i;
+    }
+    float sin2i = 1.0f - sqr(cos_i);
+    float sin2t = sin2i / sqr(ior);
+    if (sin2t >= 1.0f) return 1.0f;
+    float cost = sqrtf(1.0f - sin2t);
+    float r_parl = (ior * cos_i - cost) / (ior * cos_i + cost);
+    float r_perp = (cos_i - ior * cost) / (cos_i + ior * cost);
+    return (sqr(r_parl) + sqr(r_perp)) / 2.0f;
+}
+__device__ __forceinline__ bool refract(f3 wi, f3 n, float eta, float& etap, f3& wt) {  // :68-92
+    float cos_i = dot(n, wi);
+    if (cos_i < 0.0f) {
+        eta = 1.0f / eta;
+        cos_i = -cos_i;
+        n = -n;
+    }
+    float sin2i = gmax(0.0f, 1.0f - sqr(cos_i));
+    float sin2t = sin2i / sqr(eta);
+    if (sin2t >= 1.0f) return false;
+    float cost = sqrtf(1.0f - sin2t);
+    float k = cos_i / eta - cost;
+    wt = ((-wi) / eta) + k * n;
+    etap = eta;
+    return true;
+}
+// glm::faceforward(-normalize(wm), (0,0,1), normalize(wm))
+__device__ __forceinline__ f3 faceforward_z(f3 wm) {
+    f3 n = normalize(wm);
+    return (dot(n, mk(0.0f, 0.0f, 1.0f)) < 0.0f) ? -n : n;
+}
+__device__ __forceinline__ float dielectric_f(float roughness, f3 wo, f3 wi, int mode) {  // :96-139
+    const float eta = 1.5f;
+    float alpha = sqr(roughness);
+    if (alpha < 1e-3f) return 0.0f;
+    float co = wo.z, ci = wi.z;
+    bool reflect = ci * co > 0.0f;
+    float etap = 1.0f;
+    if (!reflect) etap = co > 0.0f ? eta : (1.0f / eta);
+    f3 wm = wi * etap + wo;
+    if (ci == 0.0f || co == 0.0f || sqr(length(wm)) == 0.0f) return 0.0f;
+    wm = faceforward_z(wm);
+    if (dot(wm, wi) * ci < 0.0f || dot(wm, wo) * co < 0.0f) return 0.0f;
+    float F = fresnel_dielectric(dot(wo, wm), eta);
+    if (reflect) return tr_D(wm, alpha) * tr_G(wo, wi, alpha) * F / fabsf(4.0f * ci * co);
+    float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap) * ci * co;
+    float ft = tr_D(wm, alpha) * (1.0f - F) * tr_G(wo, wi, alpha) * fabsf(dot(wi, wm) * dot(wo, wm) / denom);
+    if (mode == kRadiance) ft /= sqr(etap);
+    return ft;
+}
+__device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughness, f3 wo, BSample& s,
+                                                  int mode, bool reflection, bool transmission) {
+    // :146-288
+    const float eta = 1.5f;
+    float alpha = sqr(roughness);
+    float uc = rnd(seed);  // drawn first, always (:149)
+    if (alpha < 1e-3f) {
+        float R = fresnel_dielectric(wo.z, eta);
+        float T = 1.0f - R;
+        float pr = R, pt = T;
+        if (!reflection) pr = 0.0f;
+        if (!transmission) pt = 0.0f;
+        if (pr == 0.0f && pt == 0.0f) return false;
+        if (uc < pr / (pr + pt)) {
+            f3 wi = mk(-wo.x, -wo.y, wo.z);
+            float fr = R / abs_cos_theta(wi);
+            s.color = mk(fr, fr, fr);
+            s.dir = wi;
+            s.pdf = pr / (pr + pt);
+            s.refl = true;
+            s.trans = false;
+            s.spec = true;
+            return true;
+        }
+        f3 wi;
+        float etap;
+        if (!refract(wo, mk(0.0f, 0.0f, 1.0f), eta, etap, wi)) return false;
+        float ft = T / abs_cos_theta(wi);
+        if (mode == kRadiance) ft /= sqr(etap);
+        s.color = mk(ft, ft, ft);
+        s.dir = wi;
+        s.pdf = pt / (pr + pt);
+        s.refl = false;
+        s.trans = true;
+        s.spec = true;
+        return true;
+    }
+    f3 wm = tr_sample_wm(seed, wo, alpha);
+    float R = fresnel_dielectric(dot(wo, wm), eta);
+    float T = 1.0f - R;
+    float pr = R, pt = T;
+    if (!reflection) pr = 0.0f;
+    if (!transmission) pt = 0.0f;
+    if (pr == 0.0f && pt == 0.0f) return false;
+    if (uc < pr / (pr + pt)) {
+        f3 I = -wo;  // glm::reflect(I, N) = I - N*dot(N,I)*2
+        float d = dot(wm, I);
+        f3 wi = mk(I.x - wm.x * d * 2.0f, I.y - wm.y * d * 2.0f, I.z - wm.z * d * 2.0f);
+        if (!same_hemisphere(wo, wi)) return false;
+        float pdf = tr_pdf(wo, wm, alpha) / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
+        float f = tr_D(wm, alpha) * tr_G(wo, wi, alpha) * R / (4.0f * wi.z * wo.z);
+        s.color = mk(f, f, f);
+        s.dir = wi;
+        s.pdf = pdf;
+        s.refl = true;
+        s.trans = false;
+        s.spec = false;
+        return true;
+    }
+    float etap = 1.0f;
+    f3 wi = mk(0, 0, 0);
+    bool tir = !refract(wo, wm, eta, etap, wi);
+    if (tir || same_hemisphere(wo, wi) || wi.z == 0.0f) return false;
+    float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
+    float dwm_dwi = abs_dot(wi, wm) / denom;
+    float pdf = tr_pdf(wo, wm, alpha) * dwm_dwi * pt / (pr + pt);
+    float ft = T * tr_D(wm, alpha) * tr_G(wo, wi, alpha) * fabsf(dot(wi, wm) * dot(wo, wm) / (wi.z * wo.z * denom));
+    if (mode == kRadiance) ft /= sqr(etap);
+    s.color = mk(ft, ft, ft);
+    s.dir = wi;
+    s.pdf = pdf;
+    s.refl = false;
+    s.trans = true;
+    s.spec = false;
+    return true;
+}
+__device__ __forceinline__ float dielectric_pdf(float roughness, f3 wo, f3 wi, bool reflection,
+                                                bool transmission) {  // :290-343
+    const float eta = 1.5f;
+    float alpha = sqr(roughness);
+    if (alpha < 1e-3f) return 0.0f;
+    float co = wo.z, ci = wi.z;
+    bool reflect = ci * co > 0.0f;
+    float etap = 1.0f;
+    if (!reflect) etap = co > 0.0f ? eta : (1.0f / eta);
+    f3 wm = wi * etap + wo;
+    if (ci == 0.0f || co == 0.0f || length_sqr(wm) == 0.0f) return 0.0f;
+    wm = faceforward_z(wm);
+    if (dot(wm, wi) * ci < 0.0f || dot(wm, wo) * co < 0.0f) return 0.0f;
+    float R = fresnel_dielectric(dot(wo, wm), eta);
+    float T = 1.0f - R;
+    float pr = R, pt = T;
+    if (!reflection) pr = 0.0f;
+    if (!transmission) pt = 0.0f;
+    if (pr == 0.0f && pt == 0.0f) return 0.0f;
+    if (reflect) return tr_pdf(wo, wm, alpha) / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
+    float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
+    float dwm_dwi = abs_dot(wi, wm) / denom;
+    return tr_pdf(wo, wm, alpha) * dwm_dwi * pt / (pr + pt);
+}
+
+// ---- Layered "GlossyDiffuse" (dielectric top, Lambert bottom): GlossyDiffuse.h:91-524 ------
+__device__ __forceinline__ float power_heuristic(float fpdf, float gpdf) {  // :91-95 (nf=ng=1)
+    float f = 1.0f * fpdf, g = 1.0f * gpdf;
+    return sqr(f) / (sqr(f) + sqr(g));
+}
+__device__ __forceinline__ float transmittance(float dz, f3 w) {  // :97-105
+    if (gabs(dz) <= 1.17549435e-38f) return 1.0f;
+    return expf(-gabs(dz / w.z));
+}
+__device__ __forceinline__ f3 layer_f(bool top, f3 albedo, float roughness, f3 wo, f3 wi, int mode) {
+    if (top) {
+        float v = dielectric_f(roughness, wo, wi, mode);
+        return mk(v, v, v);
+    }
+    return lambert_f(albedo, wo, wi);
+}
+__device__ __forceinline__ bool layer_sample(bool top, uint32_t& seed, f3 albedo, float roughness, f3 wo,
+                                             BSample& s, int mode, bool refl, bool trans) {
+    if (top) return dielectric_sample(seed, roughness, wo, s, mode, refl, trans);
+    return lambert_sample(seed, albedo, refl, s);
+}
+__device__ __forceinline__ float layer_pdf(bool top, float roughness, f3 wo, f3 wi, bool refl, bool trans) {
+    return top ? dielectric_pdf(roughness, wo, wi, refl, trans) : lambert_pdf(wo, wi, refl);
+}
+__device__ __forceinline__ bool bs_bad(bool ok, const BSample& b) {
+    return !ok || is_zero(b.color) || b.pdf == 0.0f || b.dir.z == 0.0f;
+}
+__device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / pdf
+    float c = abs_cos_theta(b.dir);
+    return mk(b.color.x * c / b.pdf, b.color.y * c / b.pdf, b.color.z * c / b.pdf);
+}
+
+__device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+    // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code)
+    const int mode = kRadiance;
+    const float thickness = 0.01f;
+    const bool topSpec = sqr(roughness) < 1e-3f;
+    const bool botSpec = false;
+    f3 f = mk(0, 0, 0);
+    if (wo.z < 0.0f) {
+        wo = -wo;
+        wi = -wi;
+    }
+    const bool enteredTop = true;
+    const bool same = same_hemisphere(wo, wi);
+    bool exitTop, nonExitTop, exitSpec, nonExitSpec;
+    if (same ^ enteredTop) {
+        exitSpec = botSpec; nonExitSpec = topSpec; exitTop = false; nonExitTop = true;
+    } else {
+        exitSpec = topSpec; nonExitSpec = botSpec; exitTop = true; nonExitTop = false;
+    }
+    const float exitZ = (same ^ enteredTop) ? 0.0f : thickness;
+    if (same) f = mk(5.0f, 5.0f, 5.0f) * layer_f(enteredTop, albedo, roughness, wo, wi, mode);
+
+    uint32_t ns = tea16(f2u_sat(wo.x * 1000.0f), f2u_sat(wo.y * 1000.0f));
+    ns = tea16(ns, f2u_sat(wi.x * 1000.0f));
+    ns = tea16(ns, f2u_sat(wi.y * 1000.0f));
+    ns = tea16(ns, seed);
+
+    for (int s = 0; s < 5; ++s) {
+        BSample wos, wis, bs;
+        bool ok = layer_sample(enteredTop, seed, albedo, roughness, wo, wos, mode, false, true);
+        if (bs_bad(ok, wos)) continue;
+        ok = layer_sample(exitTop, seed, albedo, roughness, wi, wis, kImportance, false, true);
+        if (bs_bad(ok, wis)) continue;
+        f3 beta = bs_weight(wos);
+        float z = enteredTop ? thickness : 0.0f;
+        f3 w = wos.dir;
+        for (int depth = 0; depth < 10; ++depth) {
+            if (depth > 3 && save_max(beta) < 0.25f) {
+                float q = gmax(0.0f, 1.0f - save_max(beta));
+                if (rnd(ns) < q) break;
+                beta = beta / (1.0f - q);
+            }
+            z = (z == thickness) ? 0.0f : thickness;
+            beta = beta * transmittance(thickness, w);
+            if (z == exitZ) {
+                ok = layer_sample(exitTop, seed, albedo, roughness, -w, bs, mode, true, false);
+                if (bs_bad(ok, bs)) break;
+                beta = beta * bs_weight(bs);
+                w = bs.dir;
+            } else {
+                if (!nonExitSpec) {
+                    float wt = 1.0f;
+                    if (!exitSpec)
+                        wt = power_heuristic(wis.pdf, layer_pdf(nonExitTop, roughness, -w, -wis.dir, true, true));
+                    f3 lf = layer_f(nonExitTop, albedo, roughness, -w, -wis.dir, mode);
+                    float ac = abs_cos_theta(wis.dir);
+                    float tr = transmittance(thickness, wis.dir);
+                    f3 t1 = beta * lf;
+                    t1 = t1 * ac;
+                    t1 = t1 * wt;
+                    t1 = t1 * tr;
+                    t1 = t1 * wis.color;
+                    t1 = t1 / wis.pdf;
+                    f = f + t1;
+                }
+                ok = layer_sample(nonExitTop, seed, albedo, roughness, -w, bs, mode, true, false);
+                if (bs_bad(ok, bs)) break;
+                beta = beta * bs_weight(bs);
+                w = bs.dir;
+                if (!exitSpec) {
+                    f3 fExit = layer_f(exitTop, albedo, roughness, -w, wi, mode);
+                    if (!is_zero(fExit)) {
+                        float wt = 1.0f;
+                        if (!nonExitSpec) wt = power_heuristic(bs.pdf, layer_pdf(exitTop, roughness, -w, wi, false, true));
+                        float tr = transmittance(thickness, bs.dir);
+                        f3 t1 = beta * tr;
+                        t1 = t1 * fExit;
+                        t1 = t1 * wt;
+                        f = f + t1;
+                    }
+                }
+            }
+        }
+    }
+    return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
+}
+
+__device__ __noinline__ bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+    // GlossyDiffuse.h:372-524
+    const int mode = kRadiance;
+    const float thickness = 0.01f;
+    bool flipWi = false;
+    if (wo.z < 0.0f) {
+        wo = -wo;
+        flipWi = true;
+    }
+    BSample bs;
+    bool ok = layer_sample(true, seed, albedo, roughness, wo, bs, mode, true, true);
+    if (bs_bad(ok, bs)) return false;
+    if (bs.refl) {
+        if (flipWi) bs.dir = -bs.dir;
+        out = bs;
+        return true;
+    }
+    f3 w = bs.dir;
+    bool specPath = bs.spec;
+    uint32_t ns = tea16(f2u_sat(wo.x * 1000.0f), f2u_sat(wo.y * 1000.0f));
+    ns = tea16(ns, seed);
+    f3 f = bs.color * abs_cos_theta(bs.dir);
+    float pdf = bs.pdf;
+    float z = thickness;
+    for (int depth = 0; depth < 10; ++depth) {
+        float rrBeta = save_max(f) / pdf;
+        if (depth > 3 && rrBeta < 0.25f) {
+            float q = gmax(0.0f, 1.0f - rrBeta);
+            if (rnd(ns) < q) return false;
+            pdf *= 1.0f - q;
+        }
+        if (w.z == 0.0f) return false;
+        z = (z == thickness) ? 0.0f : thickness;
+        f = f * transmittance(thickness, w);
+        bool itop = (z == 0.0f) ? false : true;
+        ok = layer_sample(itop, seed, albedo, roughness, -w, bs, mode, true, true);
+        if (bs_bad(ok, bs)) return false;
+        f = f * bs.color;
+        pdf *= bs.pdf;
+        specPath = specPath && bs.spec;
+        w = bs.dir;
+        if (bs.trans) {
+            if (flipWi) w = -w;
+            out.color = f;
+            out.dir = w;
+            out.pdf = pdf;
+            out.refl = same_hemisphere(wo, w);
+            out.trans = !out.refl;
+            out.spec = specPath;
+            return true;
+        }
+        f = f * abs_cos_theta(bs.dir);
+    }
+    return false;
+}
+
+// ---- material dispatch: devicePrograms.cu:303-341 (+ commented alternatives) ---------------
+enum MaterialMode { kModeDefault = 0, kModeLambert = 1, kModeConductor = 2, kModeDielectric = 3, kModeLayered = 4 };
+
+template <int MODE>
+__device__ __forceinline__ bool bsdf_sample(uint32_t& seed, f3 albedo, float roughness, bool conductor, f3 wo,
+                                            BSample& bs) {
+    if (MODE == kModeLambert) return lambert_sample(seed, albedo, true, bs);
+    if (MODE == kModeConductor) return conductor_sample(seed, albedo, roughness, wo, bs);
+    if (MODE == kModeDielectric) return dielectric_sample(seed, roughness, wo, bs, kRadiance, true, true);
+    if (MODE == kModeLayered) return layered_sample(seed, albedo, roughness, wo, bs);
+    if (conductor) return conductor_sample(seed, albedo, roughness, wo, bs);
+    return layered_sample(seed, albedo, roughness, wo, bs);
+}
+template <int MODE>
+__device__ __forceinline__ f3 bsdf_f(uint32_t& seed, f3 albedo, float roughness, bool conductor, f3 wo, f3 wi) {
+    if (MODE == kModeLambert) return lambert_f(albedo, wo, wi);
+    if (MODE == kModeConductor) return conductor_f(albedo, roughness, wo, wi);
+    if (MODE == kModeDielectric) {
+        float v = dielectric_f(roughness, wo, wi, kRadiance);
+        return mk(v, v, v);
+    }
+    if (MODE == kModeLayered) return layered_f(seed, albedo, roughness, wo, wi);
+    if (conductor) return conductor_f(albedo, roughness, wo, wi);
+    return layered_f(seed, albedo, roughness, wo, wi);
+}
+
+}  // namespace pt

@@ -1,0 +1,582 @@
+// pt_capi.cpp — the C ABI of libptamd.so (include/ptamd.h): host driver for the gfx950
+// path tracer.  Replaces Renderer/OptiX/OptixRenderer.{h,cpp} of Damo12320/OptixPathtracer
+// (context/module/pipeline/SBT setup collapse into: upload scene -> LBVH build -> launch).
+//
+// There is no CPU fallback: every render and trace call runs the HIP kernels or fails
+// with a negative status.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ptamd.h"
+#include "pt_internal.h"
+
+using namespace pt;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* where) {
+    g_last_error = std::string(where) + ": " + hipGetErrorString(e);
+    return PT_ERR_HIP;
+}
+
+#define PT_HIP(call, where)                              \
+    do {                                                 \
+        hipError_t e__ = (call);                         \
+        if (e__ != hipSuccess) return hip_fail(e__, where); \
+    } while (0)
+
+// glm mat4 * vec4 for the host-side pre-transform (GetVertices, devicePrograms.cu:77-81)
+void xform4(const float* m, const float v[4], float out[4]) { mat4_mul_vec4(m, v, out); }
+
+}  // namespace
+
+struct pt_renderer {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // scene
+    BNode* d_nodes = nullptr;
+    float4* d_tri = nullptr;
+    float4* d_nrm = nullptr;
+    float4* d_mats = nullptr;
+    int ntri = 0;
+    int nmesh = 0;
+    // launch state (LaunchParams.h:9-28)
+    int width = 0, height = 0;
+    float cam_pos[3] = {0, 0, 0};
+    float inv_view[16] = {0};
+    float inv_proj[16] = {0};
+    DevLight* d_lights = nullptr;
+    int n_lights = 0;
+    int lights_cap = 0;
+    int max_bounces = 0;
+    int material_mode = PT_MAT_DEFAULT;
+    int kernel = PT_KERNEL_MEGA;
+    uint32_t frame_id = 0;
+    // buffers
+    float* d_frame = nullptr;   // 1-spp frame (pt_render)
+    float* d_accum = nullptr;   // internal sum buffer
+    float* user_accum = nullptr;
+    unsigned long long* d_counters = nullptr;
+    // stats
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool pending = false;
+    uint64_t samples = 0;
+    double last_ms = 0.0, total_ms = 0.0;
+    uint64_t calls = 0;
+    double bvh_ms = 0.0;
+    int frames_per_launch = 8;
+
+    DevScene scene() const {
+        DevScene S;
+        S.nodes = d_nodes;
+        S.tri = d_tri;
+        S.nrm = d_nrm;
+        S.mats = d_mats;
+        S.ntri = ntri;
+        return S;
+    }
+    float* accum() const { return user_accum ? user_accum : d_accum; }
+};
+
+namespace {
+
+int collect_pending(pt_renderer* r) {
+    if (!r->pending) return PT_OK;
+    PT_HIP(hipEventSynchronize(r->ev1), "hipEventSynchronize");
+    float ms = 0.0f;
+    PT_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1), "hipEventElapsedTime");
+    r->last_ms = ms;
+    r->total_ms += ms;
+    r->pending = false;
+    return PT_OK;
+}
+
+DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, uint32_t n_frames) {
+    DevLaunch L;
+    L.width = r->width;
+    L.height = r->height;
+    std::memcpy(L.cam_pos, r->cam_pos, sizeof L.cam_pos);
+    std::memcpy(L.inv_view, r->inv_view, sizeof L.inv_view);
+    std::memcpy(L.inv_proj, r->inv_proj, sizeof L.inv_proj);
+    L.lights = r->d_lights;
+    L.n_lights = r->n_lights;
+    L.max_bounces = r->max_bounces;
+    L.frame_base = frame_base;
+    L.n_frames = n_frames;
+    L.accum = accum;
+    L.counters = r->d_counters;
+    return L;
+}
+
+// Launch frames [first, first+n) in chunks, adding into accum; brackets with events.
+int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
+    int rc = collect_pending(r);
+    if (rc) return rc;
+    const DevScene S = r->scene();
+    PT_HIP(hipEventRecord(r->ev0, r->stream), "hipEventRecord");
+    uint32_t done = 0;
+    const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
+    while (done < n) {
+        uint32_t k = std::min(chunk, n - done);
+        DevLaunch L = make_launch(r, accum, first + done, k);
+        PT_HIP(launch_render(r->kernel, r->material_mode, S, L, r->stream), "render launch");
+        done += k;
+    }
+    PT_HIP(hipEventRecord(r->ev1, r->stream), "hipEventRecord");
+    r->pending = true;
+    r->samples += (uint64_t)n * (uint64_t)r->width * (uint64_t)r->height;
+    r->calls++;
+    return PT_OK;
+}
+
+bool valid_mode(int m) { return m >= PT_MAT_DEFAULT && m <= PT_MAT_LAYERED; }
+
+}  // namespace
+
+extern "C" {
+
+const char* pt_last_error(void) { return g_last_error.c_str(); }
+const char* pt_version(void) { return "ptamd 0.1.0 gfx950"; }
+
+int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** out) {
+    if (!out) return fail(PT_ERR_INVALID, "pt_create: out is NULL");
+    *out = nullptr;
+    if (!scene || scene->n_meshes < 0 || (scene->n_meshes > 0 && !scene->meshes))
+        return fail(PT_ERR_INVALID, "pt_create: invalid scene");
+    pt_options opt{};
+    if (options) opt = *options;
+    if (!valid_mode(opt.material_mode)) return fail(PT_ERR_INVALID, "pt_create: invalid material_mode");
+    if (opt.kernel != PT_KERNEL_MEGA && opt.kernel != PT_KERNEL_WAVEFRONT)
+        return fail(PT_ERR_INVALID, "pt_create: invalid kernel");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return fail(PT_ERR_HIP, "pt_create: no HIP device available");
+    if (opt.device < 0 || opt.device >= ndev) return fail(PT_ERR_INVALID, "pt_create: device out of range");
+    PT_HIP(hipSetDevice(opt.device), "hipSetDevice");
+
+    // ---- host: world-space triangle soup in original (mesh-concatenated) order ----
+    size_t ntri = 0;
+    for (int m = 0; m < scene->n_meshes; ++m) {
+        const pt_mesh& me = scene->meshes[m];
+        if (me.n_triangles < 0 || me.n_vertices < 0) return fail(PT_ERR_INVALID, "pt_create: negative counts");
+        if (me.n_triangles > 0 && (!me.vertices || !me.indices))
+            return fail(PT_ERR_INVALID, "pt_create: mesh without vertices/indices");
+        ntri += (size_t)me.n_triangles;
+    }
+    if (ntri > (size_t)0x3fffffff) return fail(PT_ERR_INVALID, "pt_create: too many triangles");
+    std::vector<float4> tri(3 * ntri), nrm(3 * ntri);
+    std::vector<float4> mats(2 * (size_t)std::max(1, scene->n_meshes));
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    size_t t = 0;
+    for (int m = 0; m < scene->n_meshes; ++m) {
+        const pt_mesh& me = scene->meshes[m];
+        mats[2 * m] = make_float4(me.albedo[0], me.albedo[1], me.albedo[2], me.metallic);
+        mats[2 * m + 1] = make_float4(me.roughness, me.normals ? 1.0f : 0.0f, 0.0f, 0.0f);
+        // world-space vertices (modelMatrix * vec4(v,1)); normals pre-transformed with w = 0
+        std::vector<float> wv(3 * (size_t)me.n_vertices), wn(3 * (size_t)me.n_vertices, 0.0f);
+        for (int v = 0; v < me.n_vertices; ++v) {
+            float in4[4] = {me.vertices[3 * v], me.vertices[3 * v + 1], me.vertices[3 * v + 2], 1.0f}, o4[4];
+            xform4(me.model_matrix, in4, o4);
+            wv[3 * v] = o4[0];
+            wv[3 * v + 1] = o4[1];
+            wv[3 * v + 2] = o4[2];
+            if (me.normals) {
+                float n4[4] = {me.normals[3 * v], me.normals[3 * v + 1], me.normals[3 * v + 2], 0.0f};
+                xform4(me.model_matrix, n4, o4);
+                wn[3 * v] = o4[0];
+                wn[3 * v + 1] = o4[1];
+                wn[3 * v + 2] = o4[2];
+            }
+        }
+        for (int i = 0; i < me.n_triangles; ++i, ++t) {
+            float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int k = 0; k < 3; ++k) {
+                int vi = me.indices[3 * i + k];
+                if (vi < 0 || vi >= me.n_vertices) return fail(PT_ERR_INVALID, "pt_create: index out of range");
+                float wbits;
+                int tag = (k == 0) ? (int)t : (k == 1 ? m : 0);
+                std::memcpy(&wbits, &tag, 4);
+                tri[3 * t + k] = make_float4(wv[3 * vi], wv[3 * vi + 1], wv[3 * vi + 2], wbits);
+                nrm[3 * t + k] = make_float4(wn[3 * vi], wn[3 * vi + 1], wn[3 * vi + 2], 0.0f);
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::min(lo[a], wv[3 * vi + a]);
+                    hi[a] = std::max(hi[a], wv[3 * vi + a]);
+                }
+            }
+            for (int a = 0; a < 3; ++a) {
+                float c = 0.5f * (lo[a] + hi[a]);
+                cmin[a] = std::min(cmin[a], c);
+                cmax[a] = std::max(cmax[a], c);
+            }
+        }
+    }
+
+    pt_renderer* r = new pt_renderer();
+    r->device = opt.device;
+    r->material_mode = opt.material_mode;
+    r->kernel = opt.kernel;
+    r->ntri = (int)ntri;
+    r->nmesh = scene->n_meshes;
+    auto cleanup_fail = [&](int code) {
+        pt_destroy(r);
+        return code;
+    };
+#define PT_HIPC(call, where)                                         \
+    do {                                                             \
+        hipError_t e__ = (call);                                     \
+        if (e__ != hipSuccess) return cleanup_fail(hip_fail(e__, where)); \
+    } while (0)
+    PT_HIPC(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking), "hipStreamCreate");
+    PT_HIPC(hipEventCreate(&r->ev0), "hipEventCreate");
+    PT_HIPC(hipEventCreate(&r->ev1), "hipEventCreate");
+    PT_HIPC(hipMalloc(&r->d_counters, 4 * sizeof(unsigned long long)), "hipMalloc counters");
+    PT_HIPC(hipMemsetAsync(r->d_counters, 0, 4 * sizeof(unsigned long long), r->stream), "hipMemset");
+    PT_HIPC(hipMalloc(&r->d_mats, sizeof(float4) * mats.size()), "hipMalloc mats");
+    PT_HIPC(hipMemcpyAsync(r->d_mats, mats.data(), sizeof(float4) * mats.size(), hipMemcpyHostToDevice, r->stream),
+            "upload mats");
+    if (ntri > 0) {
+        float4 *d_tri_orig = nullptr, *d_nrm_orig = nullptr;
+        PT_HIPC(hipMalloc(&r->d_tri, sizeof(float4) * 3 * ntri), "hipMalloc tri");
+        PT_HIPC(hipMalloc(&r->d_nrm, sizeof(float4) * 3 * ntri), "hipMalloc nrm");
+        PT_HIPC(hipMalloc(&r->d_nodes, sizeof(BNode) * std::max<size_t>(1, ntri - 1)), "hipMalloc nodes");
+        PT_HIPC(hipMalloc(&d_tri_orig, sizeof(float4) * 3 * ntri), "hipMalloc tri_orig");
+        PT_HIPC(hipMalloc(&d_nrm_orig, sizeof(float4) * 3 * ntri), "hipMalloc nrm_orig");
+        PT_HIPC(hipMemcpyAsync(d_tri_orig, tri.data(), sizeof(float4) * 3 * ntri, hipMemcpyHostToDevice, r->stream),
+                "upload tri");
+        PT_HIPC(hipMemcpyAsync(d_nrm_orig, nrm.data(), sizeof(float4) * 3 * ntri, hipMemcpyHostToDevice, r->stream),
+                "upload nrm");
+        BuildInput in;
+        in.tri_orig = d_tri_orig;
+        in.nrm_orig = d_nrm_orig;
+        in.n = (int)ntri;
+        for (int a = 0; a < 3; ++a) {
+            in.cmin[a] = cmin[a];
+            in.cmax[a] = cmax[a];
+        }
+        BuildOutput bo;
+        bo.nodes = r->d_nodes;
+        bo.tri = r->d_tri;
+        bo.nrm = r->d_nrm;
+        float ms = 0.0f;
+        hipError_t be = lbvh_build(in, bo, r->stream, &ms);
+        (void)hipStreamSynchronize(r->stream);
+        (void)hipFree(d_tri_orig);
+        (void)hipFree(d_nrm_orig);
+        if (be != hipSuccess) return cleanup_fail(hip_fail(be, "lbvh_build"));
+        r->bvh_ms = ms;
+    }
+    PT_HIPC(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+#undef PT_HIPC
+    *out = r;
+    return PT_OK;
+}
+
+int pt_destroy(pt_renderer* r) {
+    if (!r) return PT_OK;
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    (void)hipSetDevice(r->device);
+    if (r->d_nodes) (void)hipFree(r->d_nodes);
+    if (r->d_tri) (void)hipFree(r->d_tri);
+    if (r->d_nrm) (void)hipFree(r->d_nrm);
+    if (r->d_mats) (void)hipFree(r->d_mats);
+    if (r->d_lights) (void)hipFree(r->d_lights);
+    if (r->d_frame) (void)hipFree(r->d_frame);
+    if (r->d_accum) (void)hipFree(r->d_accum);
+    if (r->d_counters) (void)hipFree(r->d_counters);
+    if (r->ev0) (void)hipEventDestroy(r->ev0);
+    if (r->ev1) (void)hipEventDestroy(r->ev1);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+    return PT_OK;
+}
+
+int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_resize: NULL renderer");
+    if (width < 0 || height < 0) return fail(PT_ERR_INVALID, "pt_resize: negative size");
+    if (width == 0 || height == 0) return PT_OK;  // minimised window: no-op (OptixRenderer.cpp:651)
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    size_t bytes = sizeof(float) * 3 * (size_t)width * (size_t)height;
+    if (r->d_frame) (void)hipFree(r->d_frame);
+    if (r->d_accum) (void)hipFree(r->d_accum);
+    r->d_frame = r->d_accum = nullptr;
+    PT_HIP(hipMalloc(&r->d_frame, bytes), "hipMalloc frame");
+    PT_HIP(hipMalloc(&r->d_accum, bytes), "hipMalloc accum");
+    PT_HIP(hipMemsetAsync(r->d_accum, 0, bytes, r->stream), "hipMemset accum");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    r->width = width;
+    r->height = height;
+    r->user_accum = nullptr;
+    return PT_OK;
+}
+
+int pt_set_camera(pt_renderer* r, const float position[3], const float inverse_view[16],
+                  const float inverse_projection[16]) {
+    if (!r || !position || !inverse_view || !inverse_projection) return fail(PT_ERR_INVALID, "pt_set_camera: NULL");
+    std::memcpy(r->cam_pos, position, sizeof r->cam_pos);
+    std::memcpy(r->inv_view, inverse_view, sizeof r->inv_view);
+    std::memcpy(r->inv_proj, inverse_projection, sizeof r->inv_proj);
+    return PT_OK;
+}
+
+int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count) {
+    if (!r || count < 0 || (count > 0 && !lights)) return fail(PT_ERR_INVALID, "pt_set_lights: invalid");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    if (count > r->lights_cap) {
+        PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+        if (r->d_lights) (void)hipFree(r->d_lights);
+        r->d_lights = nullptr;
+        PT_HIP(hipMalloc(&r->d_lights, sizeof(DevLight) * (size_t)count), "hipMalloc lights");
+        r->lights_cap = count;
+    }
+    if (count > 0) {
+        std::vector<DevLight> h((size_t)count);
+        for (int i = 0; i < count; ++i)
+            h[i] = DevLight{lights[i].position[0], lights[i].position[1], lights[i].position[2],
+                            lights[i].color[0],    lights[i].color[1],    lights[i].color[2]};
+        PT_HIP(hipMemcpyAsync(r->d_lights, h.data(), sizeof(DevLight) * (size_t)count, hipMemcpyHostToDevice,
+                              r->stream),
+               "upload lights");
+        PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    }
+    r->n_lights = count;
+    return PT_OK;
+}
+
+int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_max_bounces: NULL");
+    r->max_bounces = max_bounces;
+    return PT_OK;
+}
+
+int pt_set_material_mode(pt_renderer* r, int32_t mode) {
+    if (!r || !valid_mode(mode)) return fail(PT_ERR_INVALID, "pt_set_material_mode: invalid");
+    r->material_mode = mode;
+    return PT_OK;
+}
+
+int pt_set_kernel(pt_renderer* r, int32_t kernel) {
+    if (!r || (kernel != PT_KERNEL_MEGA && kernel != PT_KERNEL_WAVEFRONT))
+        return fail(PT_ERR_INVALID, "pt_set_kernel: invalid");
+    r->kernel = kernel;
+    return PT_OK;
+}
+
+int pt_render(pt_renderer* r, float* host_rgb) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_render: NULL renderer");
+    if (r->width == 0) return PT_OK;  // OptixRenderer.cpp:621
+    if (!host_rgb) return fail(PT_ERR_INVALID, "pt_render: NULL output");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    r->frame_id++;  // :623
+    size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
+    PT_HIP(hipMemsetAsync(r->d_frame, 0, bytes, r->stream), "hipMemset frame");
+    int rc = launch_frames(r, r->d_frame, r->frame_id, 1);
+    if (rc) return rc;
+    PT_HIP(hipMemcpyAsync(host_rgb, r->d_frame, bytes, hipMemcpyDeviceToHost, r->stream), "download frame");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    return collect_pending(r);
+}
+
+int pt_accum_clear(pt_renderer* r) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_accum_clear: NULL");
+    if (r->width == 0) return fail(PT_ERR_STATE, "pt_accum_clear: call pt_resize first");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
+    PT_HIP(hipMemsetAsync(r->accum(), 0, bytes, r->stream), "hipMemset accum");
+    return PT_OK;
+}
+
+int pt_render_frames(pt_renderer* r, uint32_t first_frame_id, uint32_t n_frames) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_render_frames: NULL");
+    if (r->width == 0) return fail(PT_ERR_STATE, "pt_render_frames: call pt_resize first");
+    if (n_frames == 0) return PT_OK;
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    return launch_frames(r, r->accum(), first_frame_id, n_frames);
+}
+
+int pt_set_accum_device_buffer(pt_renderer* r, float* device_sum_rgb) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_accum_device_buffer: NULL");
+    r->user_accum = device_sum_rgb;
+    return PT_OK;
+}
+
+float* pt_accum_device_ptr(pt_renderer* r) { return r ? r->accum() : nullptr; }
+
+int pt_accum_download(pt_renderer* r, float* host_rgb, float scale) {
+    if (!r || !host_rgb) return fail(PT_ERR_INVALID, "pt_accum_download: NULL");
+    if (r->width == 0) return fail(PT_ERR_STATE, "pt_accum_download: call pt_resize first");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    size_t n = 3 * (size_t)r->width * (size_t)r->height;
+    PT_HIP(hipMemcpyAsync(host_rgb, r->accum(), n * sizeof(float), hipMemcpyDeviceToHost, r->stream), "download accum");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    if (scale != 1.0f)
+        for (size_t i = 0; i < n; ++i) host_rgb[i] *= scale;
+    return collect_pending(r);
+}
+
+int pt_synchronize(pt_renderer* r) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_synchronize: NULL");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    return collect_pending(r);
+}
+
+void* pt_stream(pt_renderer* r) { return r ? (void*)r->stream : nullptr; }
+uint32_t pt_frame_id(const pt_renderer* r) { return r ? r->frame_id : 0u; }
+int pt_set_frame_id(pt_renderer* r, uint32_t frame_id) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_frame_id: NULL");
+    r->frame_id = frame_id;
+    return PT_OK;
+}
+
+int pt_get_stats(pt_renderer* r, pt_stats* out) {
+    if (!r || !out) return fail(PT_ERR_INVALID, "pt_get_stats: NULL");
+    int rc = pt_synchronize(r);
+    if (rc) return rc;
+    unsigned long long c[4];
+    PT_HIP(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost), "download counters");
+    std::memset(out, 0, sizeof *out);
+    out->segments = c[0];
+    out->samples = r->samples;
+    out->last_render_ms = r->last_ms;
+    out->total_render_ms = r->total_ms;
+    out->render_calls = r->calls;
+    out->bvh_build_ms = r->bvh_ms;
+    out->bvh_nodes = r->ntri > 1 ? r->ntri - 1 : 0;
+    out->triangles = r->ntri;
+    return PT_OK;
+}
+
+int pt_stats_reset(pt_renderer* r) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_stats_reset: NULL");
+    int rc = pt_synchronize(r);
+    if (rc) return rc;
+    PT_HIP(hipMemset(r->d_counters, 0, 4 * sizeof(unsigned long long)), "hipMemset counters");
+    r->samples = 0;
+    r->last_ms = r->total_ms = 0.0;
+    r->calls = 0;
+    return PT_OK;
+}
+
+int pt_camera_from_blender(const float bp[3], const float br[3], float fov_deg, int32_t W, int32_t H, float pos[3],
+                           float inv_view[16], float inv_proj[16]) {
+    if (!bp || !br || !pos || !inv_view || !inv_proj || W <= 0 || H <= 0)
+        return fail(PT_ERR_INVALID, "pt_camera_from_blender: invalid");
+    const float deg2rad = 0.01745329251994329576923690768489f;  // glm::radians
+    f3 p = mk(bp[0], bp[2], -bp[1]);                             // GlmHelperMethods.cpp:4-6
+    f3 rot = mk(90.0f - br[0], 180.0f + br[2], br[1]);           // GlmHelperMethods.cpp:8-10
+    f3 rr = mk(rot.x * deg2rad, rot.y * deg2rad, rot.z * deg2rad);
+    float x = sinf(rr.y);  // Camera::GetForward, Camera.cpp:37-49
+    x *= cosf(rr.x);
+    float y = -sinf(rr.x);
+    float z = cosf(rr.x);
+    z *= cosf(rr.y);
+    f3 fwd = normalize(mk(x, y, z));
+    // glm::lookAtRH(pos, pos + fwd, (0,1,0)) — Camera.cpp:64-66
+    f3 center = p + fwd;
+    f3 f = normalize(center - p);
+    f3 s = normalize(cross(f, mk(0.0f, 1.0f, 0.0f)));
+    f3 u = cross(s, f);
+    float V[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    V[0] = s.x; V[4] = s.y; V[8] = s.z;
+    V[1] = u.x; V[5] = u.y; V[9] = u.z;
+    V[2] = -f.x; V[6] = -f.y; V[10] = -f.z;
+    V[12] = -dot(s, p); V[13] = -dot(u, p); V[14] = dot(f, p);
+    // glm::perspectiveRH_NO(fovy, aspect, 0.1, 100) — Camera.cpp:68-70, OptixRenderer.cpp:663
+    float fovy = fov_deg * deg2rad;
+    float aspect = (float)W / (float)H;
+    const float zn = 0.1f, zf = 100.0f;
+    float th = tanf(fovy / 2.0f);
+    float P[16] = {0};
+    P[0] = 1.0f / (aspect * th);
+    P[5] = 1.0f / th;
+    P[10] = -(zf + zn) / (zf - zn);
+    P[11] = -1.0f;
+    P[14] = -(2.0f * zf * zn) / (zf - zn);
+    // glm::inverse (detail/func_matrix.inl compute_inverse<4,4>)
+    auto inverse = [](const float* m, float* out) {
+        auto M = [&](int c, int r) { return m[c * 4 + r]; };
+        float C00 = M(2, 2) * M(3, 3) - M(3, 2) * M(2, 3), C02 = M(1, 2) * M(3, 3) - M(3, 2) * M(1, 3);
+        float C03 = M(1, 2) * M(2, 3) - M(2, 2) * M(1, 3), C04 = M(2, 1) * M(3, 3) - M(3, 1) * M(2, 3);
+        float C06 = M(1, 1) * M(3, 3) - M(3, 1) * M(1, 3), C07 = M(1, 1) * M(2, 3) - M(2, 1) * M(1, 3);
+        float C08 = M(2, 1) * M(3, 2) - M(3, 1) * M(2, 2), C10 = M(1, 1) * M(3, 2) - M(3, 1) * M(1, 2);
+        float C11 = M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2), C12 = M(2, 0) * M(3, 3) - M(3, 0) * M(2, 3);
+        float C14 = M(1, 0) * M(3, 3) - M(3, 0) * M(1, 3), C15 = M(1, 0) * M(2, 3) - M(2, 0) * M(1, 3);
+        float C16 = M(2, 0) * M(3, 2) - M(3, 0) * M(2, 2), C18 = M(1, 0) * M(3, 2) - M(3, 0) * M(1, 2);
+        float C19 = M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2), C20 = M(2, 0) * M(3, 1) - M(3, 0) * M(2, 1);
+        float C22 = M(1, 0) * M(3, 1) - M(3, 0) * M(1, 1), C23 = M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1);
+        const float F0[4] = {C00, C00, C02, C03}, F1[4] = {C04, C04, C06, C07}, F2[4] = {C08, C08, C10, C11};
+        const float F3[4] = {C12, C12, C14, C15}, F4[4] = {C16, C16, C18, C19}, F5[4] = {C20, C20, C22, C23};
+        const float V0[4] = {M(1, 0), M(0, 0), M(0, 0), M(0, 0)}, V1[4] = {M(1, 1), M(0, 1), M(0, 1), M(0, 1)};
+        const float V2[4] = {M(1, 2), M(0, 2), M(0, 2), M(0, 2)}, V3[4] = {M(1, 3), M(0, 3), M(0, 3), M(0, 3)};
+        const float SA[4] = {+1, -1, +1, -1}, SB[4] = {-1, +1, -1, +1};
+        float I0[4], I1[4], I2[4], I3[4];
+        for (int i = 0; i < 4; ++i) {
+            I0[i] = (V1[i] * F0[i] - V2[i] * F1[i] + V3[i] * F2[i]) * SA[i];
+            I1[i] = (V0[i] * F0[i] - V2[i] * F3[i] + V3[i] * F4[i]) * SB[i];
+            I2[i] = (V0[i] * F1[i] - V1[i] * F3[i] + V3[i] * F5[i]) * SA[i];
+            I3[i] = (V0[i] * F2[i] - V1[i] * F4[i] + V2[i] * F5[i]) * SB[i];
+        }
+        float d0 = M(0, 0) * I0[0], d1 = M(0, 1) * I1[0], d2 = M(0, 2) * I2[0], d3 = M(0, 3) * I3[0];
+        float one = 1.0f / ((d0 + d1) + (d2 + d3));
+        for (int i = 0; i < 4; ++i) {
+            out[i] = I0[i] * one;
+            out[4 + i] = I1[i] * one;
+            out[8 + i] = I2[i] * one;
+            out[12 + i] = I3[i] * one;
+        }
+    };
+    pos[0] = p.x;
+    pos[1] = p.y;
+    pos[2] = p.z;
+    inverse(V, inv_view);
+    inverse(P, inv_proj);
+    return PT_OK;
+}
+
+int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* prim, float* t, float* u, float* v,
+                  int32_t* backface, int32_t any_hit) {
+    if (!r || n < 0 || (n > 0 && (!host_rays || !prim || !t || !u || !v || !backface)))
+        return fail(PT_ERR_INVALID, "pt_trace_rays: invalid");
+    if (n == 0) return PT_OK;
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    float *d_rays = nullptr, *d_t = nullptr, *d_u = nullptr, *d_v = nullptr;
+    int *d_p = nullptr, *d_b = nullptr;
+    size_t nn = (size_t)n;
+    hipError_t e = hipMalloc(&d_rays, 8 * nn * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_t, nn * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_u, nn * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_v, nn * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_p, nn * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&d_b, nn * sizeof(int));
+    if (e == hipSuccess) e = hipMemcpyAsync(d_rays, host_rays, 8 * nn * sizeof(float), hipMemcpyHostToDevice, r->stream);
+    if (e == hipSuccess) e = launch_trace(r->scene(), d_rays, n, d_p, d_t, d_u, d_v, d_b, any_hit, r->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(prim, d_p, nn * sizeof(int), hipMemcpyDeviceToHost, r->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(t, d_t, nn * sizeof(float), hipMemcpyDeviceToHost, r->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(u, d_u, nn * sizeof(float), hipMemcpyDeviceToHost, r->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(v, d_v, nn * sizeof(float), hipMemcpyDeviceToHost, r->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(backface, d_b, nn * sizeof(int), hipMemcpyDeviceToHost, r->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_t);
+    (void)hipFree(d_u);
+    (void)hipFree(d_v);
+    (void)hipFree(d_p);
+    (void)hipFree(d_b);
+    if (e != hipSuccess) return hip_fail(e, "pt_trace_rays");
+    return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// pt_math.h — float3 arithmetic with glm 0.9.9.8 rounding order, for the gfx950 kernels.
+//
+// The reference's device code is written against glm (3rdParty/glm, used by
+// Renderer/OptiX/devicePrograms.cu and PBRT/*.h).  These helpers reproduce exactly the
+// association order of the glm functions the hot path calls (dot = (x*x'+y*y')+z*z',
+// normalize = v * (1/sqrt(dot)), cross per compute_cross, mat3*vec3 column sums), so the
+// kernels round identically to the CPU oracle (built -ffp-contract=off; the HIP sources
+// are built -ffp-contract=off as well, see Makefile).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PT_HD __host__ __device__ __forceinline__
+
+namespace pt {
+
+struct f3 {
+    float x, y, z;
+};
+
+PT_HD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+PT_HD f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+PT_HD f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+PT_HD f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+PT_HD f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+PT_HD f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+PT_HD f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+PT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+PT_HD bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+
+PT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PT_HD f3 cross(f3 a, f3 b) {
+    return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+PT_HD f3 normalize(f3 a) {
+    float i = 1.0f / sqrtf(dot(a, a));
+    return a * i;
+}
+PT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
+PT_HD float sqr(float x) { return x * x; }
+// glm::max/min/clamp on scalars (func_common.inl:17-30,505-509)
+PT_HD float gmax(float x, float y) { return (x < y) ? y : x; }
+PT_HD float gmin(float x, float y) { return (y < x) ? y : x; }
+PT_HD float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
+PT_HD float gabs(float x) { return x >= 0.0f ? x : -x; }
+PT_HD float save_max(f3 a) { return gmax(gmax(a.x, a.y), a.z); }   // glmCUDA.h:99-101
+PT_HD float abs_dot(f3 a, f3 b) { return fabsf(dot(a, b)); }       // glmCUDA.h:119-121
+PT_HD float length_sqr(f3 a) { return sqr(a.x) + sqr(a.y) + sqr(a.z); }
+
+// Shading frame: columns T, B, N (devicePrograms.cu:168-212).
+struct Frame {
+    f3 t, b, n;
+};
+// WorldToShading * v  (transpose(mat3(T,B,N)) * v)
+PT_HD f3 to_local(const Frame& f, f3 v) { return mk(dot(f.t, v), dot(f.b, v), dot(f.n, v)); }
+// ShadingToWorld * v  (glm mat3*vec3: m[0]*x + m[1]*y + m[2]*z, per row)
+PT_HD f3 to_world(const Frame& f, f3 v) {
+    return mk(f.t.x * v.x + f.b.x * v.y + f.n.x * v.z, f.t.y * v.x + f.b.y * v.y + f.n.y * v.z,
+              f.t.z * v.x + f.b.z * v.y + f.n.z * v.z);
+}
+
+// glm mat4 (column-major) * vec4: (m0*v0 + m1*v1) + (m2*v2 + m3*v3)  (type_mat4x4.inl:561-575)
+PT_HD void mat4_mul_vec4(const float* m, const float v[4], float out[4]) {
+    for (int r = 0; r < 4; ++r) {
+        float a0 = m[0 * 4 + r] * v[0];
+        float a1 = m[1 * 4 + r] * v[1];
+        float a2 = m[2 * 4 + r] * v[2];
+        float a3 = m[3 * 4 + r] * v[3];
+        out[r] = (a0 + a1) + (a2 + a3);
+    }
+}
+
+// ---- RNG: random.h:34-84 -------------------------------------------------------------
+PT_HD uint32_t tea16(uint32_t val0, uint32_t val1) {
+    uint32_t v0 = val0, v1 = val1, s0 = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++) {
+        s0 += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + s0) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + s0) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    return v0;
+}
+PT_HD float rnd(uint32_t& prev) {
+    prev = 1664525u * prev + 1013904223u;
+    return (float)(prev & 0x00FFFFFFu) / (float)0x01000000;
+}
+// PTX cvt.rzi.u32.f32 semantics (saturate, NaN -> 0) for PBRT/GlossyDiffuse.h:215-218,417-418.
+PT_HD uint32_t f2u_sat(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+
+}  // namespace pt

@@ -1,0 +1,204 @@
+"""Host-side mirror of the reference's render interface, over the C ABI.
+
+`OptixRenderer` keeps the method names and semantics of
+`Renderer/OptiX/OptixRenderer.h:63-76` (Resize, Render, SetCamera, SetLights,
+SetMaxBounces) so caller code reads like the reference's `OptixView`/`main`; the extra
+methods expose the device-resident accumulation that replaces the per-spp download + GL
+blend (`Renderer/OptixView.cpp:201-255`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import capi
+from .capi import check, fptr, load
+from .scenes import Scene
+
+
+def _f32(a, shape=None) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+class _SceneBinding:
+    """Owns the ctypes `pt_scene` and keeps every numpy buffer it points to alive."""
+
+    def __init__(self, scene: Scene):
+        self.keep = []
+        meshes = (capi.pt_mesh * max(1, len(scene.meshes)))()
+        for i, m in enumerate(scene.meshes):
+            v = _f32(m.vertices)
+            idx = np.ascontiguousarray(m.indices, dtype=np.int32)
+            self.keep += [v, idx]
+            pm = meshes[i]
+            pm.vertices = fptr(v)
+            pm.indices = idx.ctypes.data_as(C.POINTER(C.c_int32))
+            if m.normals is not None:
+                n = _f32(m.normals)
+                self.keep.append(n)
+                pm.normals = fptr(n)
+            if m.texcoords is not None:
+                t = _f32(m.texcoords)
+                self.keep.append(t)
+                pm.texcoords = fptr(t)
+            pm.n_vertices = int(v.shape[0])
+            pm.n_triangles = int(idx.shape[0])
+            pm.model_matrix[:] = [float(x) for x in _f32(m.model).ravel()]
+            pm.albedo[:] = [float(x) for x in m.albedo]
+            pm.metallic = float(m.metallic)
+            pm.roughness = float(m.roughness)
+            pm.albedo_tex = pm.normal_tex = pm.metal_rough_tex = -1
+        self.meshes = meshes
+        self.scene = capi.pt_scene()
+        self.scene.meshes = C.cast(meshes, C.POINTER(capi.pt_mesh))
+        self.scene.n_meshes = len(scene.meshes)
+        self.scene.n_textures = 0
+
+
+def camera_from_blender(pos, rot, fov_deg: float, width: int, height: int):
+    """Camera.cpp:6-70 + OptixRenderer::SetCamera: (position, inverse view, inverse projection)."""
+    lib = load()
+    p = np.empty(3, np.float32)
+    iv = np.empty(16, np.float32)
+    ip = np.empty(16, np.float32)
+    check(lib.pt_camera_from_blender(fptr(_f32(pos)), fptr(_f32(rot)), float(fov_deg), int(width), int(height),
+                                     fptr(p), fptr(iv), fptr(ip)), "pt_camera_from_blender")
+    return p, iv, ip
+
+
+class OptixRenderer:
+    """Drop-in for `OptixRenderer` (OptixRenderer.h:8-110) backed by libptamd.so."""
+
+    def __init__(self, ptx_path_or_none, model: Scene, device: int = 0, material_mode: int | None = None,
+                 kernel: int = capi.PT_KERNEL_MEGA):
+        # ptxPath is accepted for signature compatibility and ignored (no PTX on gfx950).
+        self.lib = load()
+        self.model = model
+        self._binding = _SceneBinding(model)
+        opts = capi.pt_options()
+        opts.device = int(device)
+        opts.material_mode = int(model.material_mode if material_mode is None else material_mode)
+        opts.kernel = int(kernel)
+        h = C.c_void_p()
+        check(self.lib.pt_create(C.byref(self._binding.scene), C.byref(opts), C.byref(h)), "pt_create")
+        self.h = h
+        self.size = (0, 0)
+
+    # ---- reference API --------------------------------------------------------------
+    def Resize(self, new_size) -> None:  # OptixRenderer.cpp:649-660
+        w, h = int(new_size[0]), int(new_size[1])
+        check(self.lib.pt_resize(self.h, w, h), "pt_resize")
+        if w and h:
+            self.size = (w, h)
+
+    def Render(self, h_pixels: np.ndarray | None = None) -> np.ndarray:  # :617-647
+        w, h = self.size
+        out = h_pixels if h_pixels is not None else np.zeros((h, w, 3), np.float32)
+        if w == 0:
+            return out
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == w * h * 3
+        check(self.lib.pt_render(self.h, fptr(out)), "pt_render")
+        return out
+
+    def SetCamera(self, position, inverse_view, inverse_projection) -> None:  # :662-668
+        check(self.lib.pt_set_camera(self.h, fptr(_f32(position)), fptr(_f32(inverse_view)),
+                                     fptr(_f32(inverse_projection))), "pt_set_camera")
+
+    def SetCameraBlender(self, pos, rot, fov_deg: float = 40.0) -> None:
+        w, h = self.size
+        p, iv, ip = camera_from_blender(pos, rot, fov_deg, w, h)
+        self.SetCamera(p, iv, ip)
+
+    def SetLights(self, lights) -> None:  # :670-675
+        L = _f32(lights).reshape(-1, 6)
+        arr = (capi.pt_point_light * max(1, len(L)))()
+        for i, row in enumerate(L):
+            arr[i].position[:] = [float(x) for x in row[:3]]
+            arr[i].color[:] = [float(x) for x in row[3:]]
+        check(self.lib.pt_set_lights(self.h, arr, len(L)), "pt_set_lights")
+
+    def SetMaxBounces(self, n: int) -> None:  # :677-679
+        check(self.lib.pt_set_max_bounces(self.h, int(n)), "pt_set_max_bounces")
+
+    # ---- device-resident accumulation -------------------------------------------------
+    def set_material_mode(self, mode: int) -> None:
+        check(self.lib.pt_set_material_mode(self.h, int(mode)), "pt_set_material_mode")
+
+    def set_kernel(self, kernel: int) -> None:
+        check(self.lib.pt_set_kernel(self.h, int(kernel)), "pt_set_kernel")
+
+    def accum_clear(self) -> None:
+        check(self.lib.pt_accum_clear(self.h), "pt_accum_clear")
+
+    def render_frames(self, first_frame_id: int, n_frames: int) -> None:
+        check(self.lib.pt_render_frames(self.h, int(first_frame_id), int(n_frames)), "pt_render_frames")
+
+    def set_accum_device_buffer(self, ptr: int | None) -> None:
+        check(self.lib.pt_set_accum_device_buffer(self.h, C.c_void_p(ptr) if ptr else None),
+              "pt_set_accum_device_buffer")
+
+    def accum(self, scale: float = 1.0) -> np.ndarray:
+        w, h = self.size
+        out = np.empty((h, w, 3), np.float32)
+        check(self.lib.pt_accum_download(self.h, fptr(out), float(scale)), "pt_accum_download")
+        return out
+
+    def synchronize(self) -> None:
+        check(self.lib.pt_synchronize(self.h), "pt_synchronize")
+
+    def stream(self) -> int:
+        return int(self.lib.pt_stream(self.h) or 0)
+
+    @property
+    def frame_id(self) -> int:
+        return int(self.lib.pt_frame_id(self.h))
+
+    @frame_id.setter
+    def frame_id(self, v: int) -> None:
+        check(self.lib.pt_set_frame_id(self.h, int(v)), "pt_set_frame_id")
+
+    def stats(self) -> dict:
+        s = capi.pt_stats()
+        check(self.lib.pt_get_stats(self.h, C.byref(s)), "pt_get_stats")
+        return {k: getattr(s, k) for k, _ in capi.pt_stats._fields_}
+
+    def stats_reset(self) -> None:
+        check(self.lib.pt_stats_reset(self.h), "pt_stats_reset")
+
+    def trace_rays(self, rays: np.ndarray, any_hit: bool = False):
+        """rays: (n, 8) float32 = origin, dir, tmin, tmax -> (prim, t, u, v, backface)."""
+        r = _f32(rays).reshape(-1, 8)
+        n = len(r)
+        prim = np.empty(n, np.int32)
+        t, u, v = (np.empty(n, np.float32) for _ in range(3))
+        back = np.empty(n, np.int32)
+        check(self.lib.pt_trace_rays(self.h, fptr(r), n, prim.ctypes.data_as(C.POINTER(C.c_int32)), fptr(t),
+                                     fptr(u), fptr(v), back.ctypes.data_as(C.POINTER(C.c_int32)),
+                                     1 if any_hit else 0), "pt_trace_rays")
+        return prim, t, u, v, back
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.pt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def setup_renderer(scene: Scene, width: int, height: int, max_bounces: int, device: int = 0,
+                   kernel: int = capi.PT_KERNEL_MEGA) -> OptixRenderer:
+    """The reference's main.cpp:95-113 sequence: construct, Resize, SetLights, SetMaxBounces, SetCamera."""
+    r = OptixRenderer(None, scene, device=device, kernel=kernel)
+    r.Resize((width, height))
+    r.SetLights(scene.lights)
+    r.SetMaxBounces(max_bounces)
+    r.SetCameraBlender(scene.camera_blender_pos, scene.camera_blender_rot, scene.fov_deg)
+    return r

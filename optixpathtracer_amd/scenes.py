@@ -1,0 +1,308 @@
+"""Synthetic scenes for the benchmark and parity configs (BASELINE.json `configs`).
+
+The reference's glTF test scenes are not in its repository (`.gitignore:37`), so the
+geometry here is the build's own choice, laid out after `Images/PNGs/diffuse.png` and the
+Scene1 / Scene2 presets of `OptixPathtracer/source/main.cpp:6-30`.
+Everything is generated in Blender coordinates and converted with
+`GlmHelper::BlenderToEnginePosition` (`GlmHelperMethods.cpp:4-6`): (x, y, z) -> (x, z, -y).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+IDENTITY = np.eye(4, dtype=np.float32).reshape(-1, order="F")
+
+
+@dataclass
+class Mesh:
+    """ModelLoading/Mesh.h:9-45 (vertices, normals, indices, model matrix, material)."""
+
+    vertices: np.ndarray  # (V, 3) float32
+    indices: np.ndarray  # (T, 3) int32
+    normals: np.ndarray | None = None  # (V, 3) float32
+    texcoords: np.ndarray | None = None  # (V, 2) float32
+    model: np.ndarray = field(default_factory=lambda: IDENTITY.copy())  # 16 float32, column-major
+    albedo: tuple = (1.0, 1.0, 1.0)
+    metallic: float = 0.0
+    roughness: float = 0.5
+    name: str = ""
+
+    @property
+    def n_triangles(self) -> int:
+        return int(self.indices.shape[0])
+
+
+@dataclass
+class Scene:
+    meshes: list
+    lights: np.ndarray  # (L, 6): position xyz, color rgb (engine space)
+    camera_blender_pos: tuple
+    camera_blender_rot: tuple
+    fov_deg: float = 40.0  # Camera.cpp:7 ("horizontal" FOV, used as fovy)
+    material_mode: int = 0
+    name: str = ""
+
+    @property
+    def n_triangles(self) -> int:
+        return sum(m.n_triangles for m in self.meshes)
+
+
+def blender_to_engine(p) -> np.ndarray:
+    """GlmHelperMethods.cpp:4-6: (x, y, z)_blender -> (x, z, -y)_engine."""
+    p = np.asarray(p, dtype=np.float32)
+    out = np.empty_like(p)
+    out[..., 0] = p[..., 0]
+    out[..., 1] = p[..., 2]
+    out[..., 2] = -p[..., 1]
+    return out
+
+
+def _orient(v: np.ndarray, idx: np.ndarray, want: np.ndarray) -> np.ndarray:
+    """Reorder each triangle so cross(v1-v0, v2-v0) (the CCW normal) points along `want`."""
+    a, b, c = v[idx[:, 0]], v[idx[:, 1]], v[idx[:, 2]]
+    n = np.cross(b - a, c - a)
+    flip = np.einsum("ij,ij->i", n, want) < 0
+    out = idx.copy()
+    out[flip, 1], out[flip, 2] = idx[flip, 2], idx[flip, 1]
+    return out
+
+
+def uv_sphere(center, radius: float, segments: int = 32, rings: int = 16):
+    """Blender-style UV sphere (32 segments x 16 rings = 960 triangles), outward CCW."""
+    center = np.asarray(center, dtype=np.float64)
+    verts = [center + [0.0, 0.0, radius]]
+    for i in range(1, rings):
+        th = np.pi * i / rings
+        for j in range(segments):
+            ph = 2.0 * np.pi * j / segments
+            verts.append(center + radius * np.array([np.sin(th) * np.cos(ph), np.sin(th) * np.sin(ph), np.cos(th)]))
+    verts.append(center + [0.0, 0.0, -radius])
+    v = np.array(verts)
+    top, bot = 0, len(verts) - 1
+
+    def ring(i, j):
+        return 1 + i * segments + (j % segments)
+
+    tris = []
+    for j in range(segments):
+        tris.append((top, ring(0, j), ring(0, j + 1)))
+    for i in range(rings - 2):
+        for j in range(segments):
+            a, b, c, d = ring(i, j), ring(i + 1, j), ring(i + 1, j + 1), ring(i, j + 1)
+            tris.append((a, b, c))
+            tris.append((a, c, d))
+    for j in range(segments):
+        tris.append((bot, ring(rings - 2, j + 1), ring(rings - 2, j)))
+    idx = np.array(tris, dtype=np.int64)
+    n = (v - center) / radius
+    cen = (v[idx[:, 0]] + v[idx[:, 1]] + v[idx[:, 2]]) / 3.0 - center
+    idx = _orient(v, idx, cen)
+    return v, n, idx
+
+
+def quad(p0, p1, p2, p3, normal):
+    """Two-triangle quad with a flat vertex normal; CCW around `normal`."""
+    v = np.array([p0, p1, p2, p3], dtype=np.float64)
+    idx = np.array([[0, 1, 2], [0, 2, 3]], dtype=np.int64)
+    nn = np.tile(np.asarray(normal, dtype=np.float64), (4, 1))
+    idx = _orient(v, idx, nn[:2])
+    return v, nn, idx
+
+
+def _mesh_from_blender(v, n, idx, **kw) -> Mesh:
+    return Mesh(
+        vertices=np.ascontiguousarray(blender_to_engine(v), dtype=np.float32),
+        normals=np.ascontiguousarray(blender_to_engine(n), dtype=np.float32),
+        indices=np.ascontiguousarray(idx, dtype=np.int32),
+        **kw,
+    )
+
+
+SCENE1_CAMERA = ((3.85382, 0.0, 1.0), (90.0, 0.0, 90.0))  # main.cpp:10-11
+SCENE1_LIGHTS_BLENDER = [  # main.cpp:13-17
+    (1.33906, -0.7, 0.299367),
+    (1.33906, 0.7, 0.299367),
+    (1.33906, 0.7, 1.69937),
+    (1.33906, -0.7, 1.69937),
+]
+
+VARIANTS = ("diffuse", "conductor", "dielectric20", "layered")
+
+
+def sphere_in_box(variant: str = "diffuse", sphere_segments: int = 32, sphere_rings: int = 16,
+                  grid: int = 6) -> Scene:
+    """'Diffuse sphere-in-box' (SURVEY.md §8(d)): 6x6 UV spheres (r = 0.2) in an open box.
+
+    variant:
+      diffuse      Lambert mode (config 1, 2)
+      conductor    Default mode, spheres metallic 1 (TR roughness = column/5), walls
+                   metallic 0 -> Layered (config 3)
+      dielectric20 Dielectric mode everywhere, lights x20 (config 4i)
+      layered      Layered mode everywhere (config 4ii)
+    """
+    if variant not in VARIANTS:
+        raise ValueError(f"unknown variant {variant!r}; choose from {VARIANTS}")
+    from .capi import PT_MAT_DEFAULT, PT_MAT_DIELECTRIC, PT_MAT_LAMBERT, PT_MAT_LAYERED
+
+    mode = {"diffuse": PT_MAT_LAMBERT, "conductor": PT_MAT_DEFAULT, "dielectric20": PT_MAT_DIELECTRIC,
+            "layered": PT_MAT_LAYERED}[variant]
+    sphere_metal = 1.0 if variant == "conductor" else 0.0
+    meshes = []
+    for i in range(grid):
+        for j in range(grid):
+            c = (0.0, -1.175 + 0.47 * j, -0.175 + 0.47 * i)
+            v, n, idx = uv_sphere(c, 0.2, sphere_segments, sphere_rings)
+            meshes.append(_mesh_from_blender(v, n, idx, albedo=(0.6, 0.02, 0.02), metallic=sphere_metal,
+                                             roughness=j / 5.0, name=f"sphere_{i}_{j}"))
+    # open-front box, inward normals; front edge at x = 2.4 (camera at x = 3.85 looks along -x)
+    x0, x1, y0, y1, z0, z1 = -0.6, 2.4, -1.8, 1.8, -0.6, 2.6
+    grey, green, blue = (0.5, 0.5, 0.5), (0.05, 0.4, 0.05), (0.05, 0.05, 0.4)
+    walls = [
+        ("back", [(x0, y0, z0), (x0, y1, z0), (x0, y1, z1), (x0, y0, z1)], (1, 0, 0), grey),
+        ("floor", [(x0, y0, z0), (x1, y0, z0), (x1, y1, z0), (x0, y1, z0)], (0, 0, 1), grey),
+        ("ceiling", [(x0, y0, z1), (x0, y1, z1), (x1, y1, z1), (x1, y0, z1)], (0, 0, -1), grey),
+        ("left", [(x0, y0, z0), (x0, y0, z1), (x1, y0, z1), (x1, y0, z0)], (0, 1, 0), green),
+        ("right", [(x0, y1, z0), (x1, y1, z0), (x1, y1, z1), (x0, y1, z1)], (0, -1, 0), blue),
+    ]
+    for name, pts, nrm, col in walls:
+        v, n, idx = quad(*pts, nrm)
+        meshes.append(_mesh_from_blender(v, n, idx, albedo=col, metallic=0.0, roughness=0.5, name=name))
+    scale = 20.0 if variant == "dielectric20" else 1.0
+    lights = np.array([[*blender_to_engine(p), scale, scale, scale] for p in SCENE1_LIGHTS_BLENDER],
+                      dtype=np.float32)
+    return Scene(meshes=meshes, lights=lights, camera_blender_pos=SCENE1_CAMERA[0],
+                 camera_blender_rot=SCENE1_CAMERA[1], material_mode=mode, name=f"sphere_box_{variant}")
+
+
+def tiny_scene(variant: str = "diffuse") -> Scene:
+    """A few-hundred-triangle version (2x2 coarse spheres) for fast CPU-oracle parity."""
+    return sphere_in_box(variant, sphere_segments=12, sphere_rings=6, grid=2)
+
+
+# ---------------------------------------------------------------------------------------
+# "Sponza-class" procedural atrium (config 5): ~250k triangles, mixed BRDFs.
+# ---------------------------------------------------------------------------------------
+SCENE2_CAMERA = ((-0.977644, -0.366231, 1.0745), (89.1897, 0.0, 77.765))  # main.cpp:24-25
+SCENE2_LIGHT_BLENDER = (0.0, 0.0, 4.12939)  # main.cpp:28-29, colour 100
+
+
+def _cylinder(cx, cy, z0, z1, r, segs, stacks):
+    th = np.linspace(0.0, 2.0 * np.pi, segs, endpoint=False)
+    zs = np.linspace(z0, z1, stacks + 1)
+    ring = np.stack([np.cos(th), np.sin(th)], axis=1)
+    v = np.concatenate([np.column_stack([cx + r * ring[:, 0], cy + r * ring[:, 1], np.full(segs, z)]) for z in zs])
+    n = np.concatenate([np.column_stack([ring[:, 0], ring[:, 1], np.zeros(segs)]) for _ in zs])
+    tris = []
+    for k in range(stacks):
+        for j in range(segs):
+            a, b = k * segs + j, k * segs + (j + 1) % segs
+            c, d = a + segs, b + segs
+            tris += [(a, b, d), (a, d, c)]
+    idx = np.array(tris, dtype=np.int64)
+    cen = v[idx].mean(axis=1)
+    out = np.column_stack([cen[:, 0] - cx, cen[:, 1] - cy, np.zeros(len(idx))])
+    idx = _orient(v, idx, out)
+    return v, n, idx
+
+
+def _arch(x0, x1, y, zb, r_in, r_out, segs):
+    """Half-annulus arch spanning x0..x1 in the plane y, springing at height zb (front+back faces)."""
+    cx = 0.5 * (x0 + x1)
+    th = np.linspace(0.0, np.pi, segs + 1)
+    verts, norms, tris = [], [], []
+    for face, dy, sgn in ((0, -0.1, -1.0), (1, 0.1, 1.0)):
+        base = len(verts)
+        for t in th:
+            for rr in (r_in, r_out):
+                verts.append((cx + rr * np.cos(t), y + dy, zb + rr * np.sin(t)))
+                norms.append((0.0, sgn, 0.0))
+        for k in range(segs):
+            a = base + 2 * k
+            tris += [(a, a + 1, a + 3), (a, a + 3, a + 2)]
+    v, n = np.array(verts), np.array(norms)
+    idx = np.array(tris, dtype=np.int64)
+    want = n[idx[:, 0]]
+    return v, n, _orient(v, idx, want)
+
+
+def sponza_class(seed: int = 12345, target_tris: int = 250_000) -> Scene:
+    """Procedural atrium (floor tiles, two storeys of colonnades, arches, walls): ~250k tris.
+
+    Per-object metallic in {0,1} and roughness ~ U[0,1] from `seed`.
+    Default material mode (Conductor / Layered by the metallic coin).
+    """
+    rng = np.random.default_rng(seed)
+    from .capi import PT_MAT_DEFAULT
+
+    meshes = []
+
+    def add(v, n, idx, name):
+        metallic = float(rng.integers(0, 2))
+        rough = float(rng.uniform(0.0, 1.0))
+        alb = tuple(float(a) for a in rng.uniform(0.2, 0.9, size=3))
+        meshes.append(_mesh_from_blender(v, n, idx, albedo=alb, metallic=metallic, roughness=rough, name=name))
+
+    L, W = 12.0, 5.0  # half length (x), half width (y)
+    # tiled floor: 96 x 40 tiles
+    nx, ny = 96, 40
+    xs, ys = np.linspace(-L, L, nx + 1), np.linspace(-W, W, ny + 1)
+    gx, gy = np.meshgrid(xs, ys, indexing="ij")
+    v = np.column_stack([gx.ravel(), gy.ravel(), np.zeros(gx.size)])
+    n = np.tile([0.0, 0.0, 1.0], (len(v), 1))
+    tris = []
+    for i in range(nx):
+        for j in range(ny):
+            a = i * (ny + 1) + j
+            tris += [(a, a + ny + 1, a + ny + 2), (a, a + ny + 2, a + 1)]
+    idx = _orient(v, np.array(tris), np.tile([0.0, 0.0, 1.0], (len(tris), 1)))
+    add(v, n, idx, "floor")
+    # walls (outer) and gallery slabs
+    for name, pts, nrm in [
+        ("wall_s", [(-L, -W, 0), (L, -W, 0), (L, -W, 9), (-L, -W, 9)], (0, 1, 0)),
+        ("wall_n", [(-L, W, 0), (-L, W, 9), (L, W, 9), (L, W, 0)], (0, -1, 0)),
+        ("wall_w", [(-L, -W, 0), (-L, -W, 9), (-L, W, 9), (-L, W, 0)], (1, 0, 0)),
+        ("wall_e", [(L, -W, 0), (L, W, 0), (L, W, 9), (L, -W, 9)], (-1, 0, 0)),
+        ("gallery_s", [(-L, -W, 4.5), (-L, -2.5, 4.5), (L, -2.5, 4.5), (L, -W, 4.5)], (0, 0, -1)),
+        ("gallery_n", [(-L, 2.5, 4.5), (-L, W, 4.5), (L, W, 4.5), (L, 2.5, 4.5)], (0, 0, -1)),
+    ]:
+        v, n, idx = quad(*pts, nrm)
+        add(v, n, idx, name)
+    # colonnades: ground (tall) + gallery (short) columns at y = +-2.5, arches between them
+    col_x = np.linspace(-L + 1.0, L - 1.0, 16)
+    budget_used = sum(m.n_triangles for m in meshes)
+    ground_segs, ground_stacks = 48, 40
+    for y in (-2.5, 2.5):
+        for k, x in enumerate(col_x):
+            v, n, idx = _cylinder(x, y, 0.0, 3.6, 0.22, ground_segs, ground_stacks)
+            add(v, n, idx, f"col_{y}_{k}")
+            v, n, idx = _cylinder(x, y, 4.5, 7.0, 0.15, 32, 16)
+            add(v, n, idx, f"gcol_{y}_{k}")
+        for k in range(len(col_x) - 1):
+            v, n, idx = _arch(col_x[k] + 0.22, col_x[k + 1] - 0.22, y, 3.6, 0.45, 0.7, 64)
+            add(v, n, idx, f"arch_{y}_{k}")
+    budget_used = sum(m.n_triangles for m in meshes)
+    # fill the remaining budget with a field of small spheres (statues / lamps) in the court
+    k = 0
+    while budget_used + 960 <= target_tris:
+        cx = rng.uniform(-L + 1.5, L - 1.5)
+        cy = rng.uniform(-2.0, 2.0)
+        cz = rng.uniform(0.3, 3.0)
+        v, n, idx = uv_sphere((cx, cy, cz), rng.uniform(0.05, 0.25))
+        add(v, n, idx, f"orb_{k}")
+        budget_used += 960
+        k += 1
+    light = np.array([[*blender_to_engine(SCENE2_LIGHT_BLENDER), 100.0, 100.0, 100.0]], dtype=np.float32)
+    return Scene(meshes=meshes, lights=light, camera_blender_pos=SCENE2_CAMERA[0],
+                 camera_blender_rot=SCENE2_CAMERA[1], material_mode=PT_MAT_DEFAULT, name="sponza_class")
+
+
+def make_scene(name: str) -> Scene:
+    if name.startswith("sphere_box_"):
+        return sphere_in_box(name[len("sphere_box_"):])
+    if name.startswith("tiny_"):
+        return tiny_scene(name[len("tiny_"):])
+    if name == "sponza_class":
+        return sponza_class()
+    raise ValueError(f"unknown scene {name!r}")

@@ -1,0 +1,63 @@
+"""Shared helpers for the parity tests: run the same config through the HIP product (C ABI)
+and through the CPU oracle, and compare."""
+from __future__ import annotations
+
+import numpy as np
+
+
+def image_mse(a: np.ndarray, b: np.ndarray) -> float:
+    """Mean over pixels x channels of the squared difference, NaN -> 0 (the reference's EXR
+    writer zeroes NaN pixels, Renderer/Images/WriteImage.cpp:52-55)."""
+    a = np.nan_to_num(np.asarray(a, np.float64), nan=0.0)
+    b = np.nan_to_num(np.asarray(b, np.float64), nan=0.0)
+    return float(np.mean((a - b) ** 2))
+
+
+def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, kernel=0, device=0):
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    r = setup_renderer(scene, width, height, max_bounces, device=device, kernel=kernel)
+    if mode is not None:
+        r.set_material_mode(mode)
+    r.accum_clear()
+    r.render_frames(first_frame, n_frames)
+    img = r.accum()
+    st = r.stats()
+    r.close()
+    return img, st
+
+
+def oracle_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, rect=None):
+    from oracle.oracle import OracleScene
+
+    o = OracleScene(scene)
+    lp = o.launch(width, height, max_bounces, material_mode=mode)
+    img, segs = o.render(lp, first_frame, n_frames, rect=rect)
+    o.close()
+    return img, segs
+
+
+def random_rays(scene, n, seed=0, tmax=100.0):
+    """Rays from random points in the scene bounds toward random directions, plus rays aimed
+    at random triangle interiors/edges/vertices (edge and vertex hits exercise the tie rule)."""
+    rng = np.random.default_rng(seed)
+    verts = np.concatenate([m.vertices for m in scene.meshes])
+    lo, hi = verts.min(0), verts.max(0)
+    o = rng.uniform(lo - 0.5, hi + 0.5, size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    # aim a third at triangle points (vertices, edge midpoints, interiors)
+    tris = np.concatenate([m.vertices[m.indices] for m in scene.meshes])
+    k = n // 3
+    ti = rng.integers(0, len(tris), size=k)
+    w = rng.dirichlet([1.0, 1.0, 1.0], size=k)
+    w[: k // 3] = np.eye(3)[rng.integers(0, 3, size=k // 3)]  # vertices
+    w[k // 3: 2 * k // 3] = [0.5, 0.5, 0.0]  # edge midpoints
+    tgt = np.einsum("ij,ijk->ik", w, tris[ti])
+    d[:k] = tgt - o[:k]
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = o
+    rays[:, 3:6] = d
+    rays[:, 6] = 0.0
+    rays[:, 7] = tmax
+    return rays
