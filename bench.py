@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the MI355X path tracer on BASELINE.json configs[1].
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (configs[1]): the synthetic Diffuse sphere-in-box scene (34,570 triangles,
+Lambert mode, Scene1 camera and 4 point lights), 1920x1080, depth 8.  One STEP = one
+1024-spp render of the full frame per GPU: every rank renders its own disjoint frame-id
+range (spp sharding) into a device fp32 accumulator, then the
+accumulators are summed to rank 0 with one RCCL reduce (torch.distributed "nccl" = RCCL
+over xGMI).  Per-GPU work is fixed as N grows ("weak" scaling); value = all samples of
+all ranks / max-over-ranks wall time.
+
+Extra fields: `roofline` (HBM roofline of the render kernel: algorithmic bytes per launch,
+SURVEY.md §8(d) 396 B/segment + 12 B/sample, over the per-launch average measured with
+HIP events on the library stream) and `cpu_baseline` (the CPU oracle, oracle/, timed on a
+bounded band of the same workload on the host cores, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+BYTES_PER_SEGMENT = 396  # compulsory SoA queue + gather traffic per path segment
+BYTES_PER_SAMPLE = 12  # final fp32 RGB accumulate
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="sphere_box_diffuse")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024, help="samples per pixel per GPU per step")
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--kernel", type=int, default=0, help="0 = megakernel, 1 = wavefront")
+    ap.add_argument("--frames-per-launch", type=int, default=8)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
+                    help="PMC traffic per launch measured by tools/profile.sh (optional)")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, args, budget_s: float):
+    """The CPU oracle (oracle/liboracle.so, test/baseline infrastructure) on a band of the
+    same workload, on this host's cores; sized to ~budget_s of CPU work."""
+    from oracle.oracle import OracleScene
+
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    o = OracleScene(scene)
+    lp = o.launch(args.width, args.height, args.depth)
+    y0 = args.height // 2
+    # calibration band: 2 rows x 1 spp
+    t = time.perf_counter()
+    o.render(lp, 1, 1, rect=(0, y0, args.width, y0 + 2), threads=threads)
+    dt = max(time.perf_counter() - t, 1e-3)
+    per_row = dt / 2
+    rows = int(max(2, min(args.height - y0, budget_s / per_row)))
+    spp = int(max(1, min(args.spp, budget_s / (per_row * rows))))
+    t = time.perf_counter()
+    _, segs = o.render(lp, 1, spp, rect=(0, y0, args.width, y0 + rows), threads=threads)
+    dt = time.perf_counter() - t
+    samples = rows * args.width * spp
+    o.close()
+    return {
+        "value": round(samples / dt / 1e6, 4),
+        "unit": "Msamples/sec",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{rows} rows x {args.width} px x {spp} spp (frame ids 1..{spp}) of the same scene/depth, "
+                  f"rows {y0}..{y0 + rows - 1}, "
+                  f"{dt:.1f} s, {segs} segments",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    import numpy as np
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl", init_method="env://")
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    scene = scenes.make_scene(args.scene)
+    t0 = time.perf_counter()
+    r = setup_renderer(scene, args.width, args.height, args.depth, device=local_rank, kernel=args.kernel)
+    r.set_frames_per_launch(args.frames_per_launch)
+    setup_s = time.perf_counter() - t0
+    bvh_ms = r.stats()["bvh_build_ms"]
+    dev = torch.device("cuda", local_rank)
+    accum = torch.zeros((args.height, args.width, 3), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)
+    r.set_accum_device_buffer(accum.data_ptr())
+    if rank == 0:
+        log(f"[bench] scene={args.scene} tris={scene.n_triangles} {args.width}x{args.height} spp/step/gpu={args.spp} "
+            f"depth={args.depth} world={world} setup={setup_s:.2f}s lbvh={bvh_ms:.3f}ms")
+
+    def step(s: int):
+        r.accum_clear()
+        first = 1 + (s * world + rank) * args.spp  # disjoint frame ids per (step, rank)
+        r.render_frames(first, args.spp)
+        r.synchronize()
+        if dist is not None:
+            dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)  # RCCL over xGMI
+
+    for s in range(args.warmup):
+        step(s)
+        if rank == 0:
+            log(f"[bench] warmup {s + 1}/{args.warmup} done")
+    torch.cuda.synchronize(dev)
+    r.stats_reset()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s)
+        if rank == 0:
+            log(f"[bench] step {s + 1}/{args.steps} {time.perf_counter() - t0:.2f}s")
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    st = r.stats()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    samples_total = args.width * args.height * args.spp * args.steps * world
+    value = samples_total / elapsed / 1e6
+    if rank == 0:
+        img = accum.cpu().numpy()
+        nan_px = int(np.isnan(img).any(axis=-1).sum())
+        launches = max(1, int(st["kernel_launches"]))
+        kernel_s = st["total_render_ms"] / 1e3
+        alg_bytes = st["segments"] * BYTES_PER_SEGMENT + st["samples"] * BYTES_PER_SAMPLE
+        per_launch_bytes = alg_bytes / launches
+        avg_launch_s = kernel_s / launches
+        achieved = per_launch_bytes / avg_launch_s / 1e9
+        traffic = None
+        tj = Path(args.traffic_json)
+        if tj.exists():
+            try:
+                traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "Msamples/sec at 1920x1080, max-depth 8; MSE vs reference",
+            "value": round(value, 3),
+            "unit": "Msamples/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural sphere-in-box scene; reference glTF assets are not in its repo)",
+            "config": {
+                "workload": "BASELINE configs[1]: Diffuse sphere-in-box 1920x1080, 1024 spp, depth 8, 1xMI355X"
+                if world == 1 else f"BASELINE configs[1] per GPU, spp-sharded over {world} GPUs + RCCL reduce",
+                "scene": args.scene,
+                "triangles": scene.n_triangles,
+                "width": args.width,
+                "height": args.height,
+                "spp_per_gpu_per_step": args.spp,
+                "max_depth": args.depth,
+                "material_mode": "lambert" if scene.material_mode == 1 else str(scene.material_mode),
+                "kernel": "megakernel" if args.kernel == 0 else "wavefront",
+                "frames_per_launch": args.frames_per_launch,
+                "parallelism": f"spp-shard x{world}",
+                "lbvh_build_ms": round(bvh_ms, 3),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                "traffic": traffic,
+                "kernel": "k_render_mega",
+                "bytes_per_launch": int(per_launch_bytes),
+                "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "launches": launches,
+                "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
+            },
+            "image": {"mean": float(np.nanmean(img) / (args.spp * world)), "nan_pixels": nan_px},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("[bench] cpu baseline (oracle) ...")
+            out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -85,12 +85,16 @@ typedef struct pt_options {
 typedef struct pt_stats {
     uint64_t segments;        /* radiance rays traced (path segments) since pt_stats_reset */
     uint64_t samples;         /* camera paths since pt_stats_reset */
-    double last_render_ms;    /* device time of the last render call (HIP events, library stream) */
-    double total_render_ms;   /* summed device time since pt_stats_reset */
-    uint64_t render_calls;
+    double last_render_ms;    /* summed kernel time of the last render call */
+    double total_render_ms;   /* summed kernel time since pt_stats_reset */
+    uint64_t render_calls;    /* pt_render / pt_render_frames calls since pt_stats_reset */
+    uint64_t kernel_launches; /* render-kernel launches since pt_stats_reset; each one is
+                                 bracketed by its own HIP event pair on the library stream */
     double bvh_build_ms;      /* LBVH build device time (pt_create) */
     int32_t bvh_nodes;        /* internal nodes */
     int32_t triangles;
+    int32_t frames_per_launch;
+    int32_t reserved;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -113,6 +117,8 @@ int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count);
 int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces);
 int pt_set_material_mode(pt_renderer* r, int32_t material_mode);
 int pt_set_kernel(pt_renderer* r, int32_t kernel);
+/* frames (spp) rendered per kernel launch by pt_render_frames (default 8). */
+int pt_set_frames_per_launch(pt_renderer* r, int32_t frames);
 
 /* OptixRenderer::Render(glm::vec3 h_pixels[]) — OptixRenderer.cpp:617-647: frame.id++,
  * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before

@@ -80,9 +80,12 @@ class pt_stats(C.Structure):
         ("last_render_ms", C.c_double),
         ("total_render_ms", C.c_double),
         ("render_calls", C.c_uint64),
+        ("kernel_launches", C.c_uint64),
         ("bvh_build_ms", C.c_double),
         ("bvh_nodes", C.c_int32),
         ("triangles", C.c_int32),
+        ("frames_per_launch", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
@@ -100,6 +103,7 @@ SIGNATURES = {
     "pt_set_max_bounces": (C.c_int, [_R, C.c_int32]),
     "pt_set_material_mode": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel": (C.c_int, [_R, C.c_int32]),
+    "pt_set_frames_per_launch": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),
     "pt_accum_clear": (C.c_int, [_R]),
     "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),

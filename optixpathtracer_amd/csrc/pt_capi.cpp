@@ -69,8 +69,10 @@ struct pt_renderer {
     float* d_accum = nullptr;   // internal sum buffer
     float* user_accum = nullptr;
     unsigned long long* d_counters = nullptr;
-    // stats
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // stats: one HIP event pair per kernel launch, on the library stream
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    size_t ev_used = 0;
+    uint64_t launches = 0;
     bool pending = false;
     uint64_t samples = 0;
     double last_ms = 0.0, total_ms = 0.0;
@@ -94,12 +96,32 @@ namespace {
 
 int collect_pending(pt_renderer* r) {
     if (!r->pending) return PT_OK;
-    PT_HIP(hipEventSynchronize(r->ev1), "hipEventSynchronize");
-    float ms = 0.0f;
-    PT_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1), "hipEventElapsedTime");
-    r->last_ms = ms;
-    r->total_ms += ms;
+    double sum = 0.0;
+    if (r->ev_used > 0) PT_HIP(hipEventSynchronize(r->ev_stop[r->ev_used - 1]), "hipEventSynchronize");
+    for (size_t i = 0; i < r->ev_used; ++i) {
+        float ms = 0.0f;
+        PT_HIP(hipEventElapsedTime(&ms, r->ev_start[i], r->ev_stop[i]), "hipEventElapsedTime");
+        sum += ms;
+    }
+    r->launches += r->ev_used;
+    r->ev_used = 0;
+    r->last_ms = sum;
+    r->total_ms += sum;
     r->pending = false;
+    return PT_OK;
+}
+
+int next_event_pair(pt_renderer* r, hipEvent_t* a, hipEvent_t* b) {
+    if (r->ev_used == r->ev_start.size()) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        PT_HIP(hipEventCreate(&e0), "hipEventCreate");
+        PT_HIP(hipEventCreate(&e1), "hipEventCreate");
+        r->ev_start.push_back(e0);
+        r->ev_stop.push_back(e1);
+    }
+    *a = r->ev_start[r->ev_used];
+    *b = r->ev_stop[r->ev_used];
+    r->ev_used++;
     return PT_OK;
 }
 
@@ -125,17 +147,20 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
     int rc = collect_pending(r);
     if (rc) return rc;
     const DevScene S = r->scene();
-    PT_HIP(hipEventRecord(r->ev0, r->stream), "hipEventRecord");
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
+    r->pending = true;
     while (done < n) {
         uint32_t k = std::min(chunk, n - done);
         DevLaunch L = make_launch(r, accum, first + done, k);
+        hipEvent_t a, b;
+        rc = next_event_pair(r, &a, &b);
+        if (rc) return rc;
+        PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
         PT_HIP(launch_render(r->kernel, r->material_mode, S, L, r->stream), "render launch");
+        PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
         done += k;
     }
-    PT_HIP(hipEventRecord(r->ev1, r->stream), "hipEventRecord");
-    r->pending = true;
     r->samples += (uint64_t)n * (uint64_t)r->width * (uint64_t)r->height;
     r->calls++;
     return PT_OK;
@@ -239,8 +264,6 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         if (e__ != hipSuccess) return cleanup_fail(hip_fail(e__, where)); \
     } while (0)
     PT_HIPC(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking), "hipStreamCreate");
-    PT_HIPC(hipEventCreate(&r->ev0), "hipEventCreate");
-    PT_HIPC(hipEventCreate(&r->ev1), "hipEventCreate");
     PT_HIPC(hipMalloc(&r->d_counters, 4 * sizeof(unsigned long long)), "hipMalloc counters");
     PT_HIPC(hipMemsetAsync(r->d_counters, 0, 4 * sizeof(unsigned long long), r->stream), "hipMemset");
     PT_HIPC(hipMalloc(&r->d_mats, sizeof(float4) * mats.size()), "hipMalloc mats");
@@ -295,8 +318,8 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_counters) (void)hipFree(r->d_counters);
-    if (r->ev0) (void)hipEventDestroy(r->ev0);
-    if (r->ev1) (void)hipEventDestroy(r->ev1);
+    for (hipEvent_t e : r->ev_start) (void)hipEventDestroy(e);
+    for (hipEvent_t e : r->ev_stop) (void)hipEventDestroy(e);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
     return PT_OK;
@@ -453,6 +476,8 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->last_render_ms = r->last_ms;
     out->total_render_ms = r->total_ms;
     out->render_calls = r->calls;
+    out->kernel_launches = r->launches;
+    out->frames_per_launch = r->frames_per_launch;
     out->bvh_build_ms = r->bvh_ms;
     out->bvh_nodes = r->ntri > 1 ? r->ntri - 1 : 0;
     out->triangles = r->ntri;
@@ -467,6 +492,13 @@ int pt_stats_reset(pt_renderer* r) {
     r->samples = 0;
     r->last_ms = r->total_ms = 0.0;
     r->calls = 0;
+    r->launches = 0;
+    return PT_OK;
+}
+
+int pt_set_frames_per_launch(pt_renderer* r, int32_t frames) {
+    if (!r || frames < 1) return fail(PT_ERR_INVALID, "pt_set_frames_per_launch: invalid");
+    r->frames_per_launch = frames;
     return PT_OK;
 }
 

@@ -131,6 +131,9 @@ class OptixRenderer:
     def set_kernel(self, kernel: int) -> None:
         check(self.lib.pt_set_kernel(self.h, int(kernel)), "pt_set_kernel")
 
+    def set_frames_per_launch(self, frames: int) -> None:
+        check(self.lib.pt_set_frames_per_launch(self.h, int(frames)), "pt_set_frames_per_launch")
+
     def accum_clear(self) -> None:
         check(self.lib.pt_accum_clear(self.h), "pt_accum_clear")
 
