@@ -124,13 +124,14 @@ def main():
         log(f"[bench] scene={args.scene} tris={scene.n_triangles} {args.width}x{args.height} spp/step/gpu={args.spp} "
             f"depth={args.depth} world={world} setup={setup_s:.2f}s lbvh={bvh_ms:.3f}ms")
 
+    from optixpathtracer_amd import sharding
+
     def step(s: int):
         r.accum_clear()
-        first = 1 + (s * world + rank) * args.spp  # disjoint frame ids per (step, rank)
-        r.render_frames(first, args.spp)
+        first, n = sharding.frame_range(s, rank, world, args.spp)  # disjoint frame ids per (step, rank)
+        r.render_frames(first, n)
         r.synchronize()
-        if dist is not None:
-            dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)  # RCCL over xGMI
+        sharding.reduce_accumulator(accum, dist)  # RCCL over xGMI
 
     for s in range(args.warmup):
         step(s)

@@ -1,0 +1,29 @@
+"""spp sharding across GPUs.
+
+Every (pixel, frame id) sample is independent and seeded by tea<16>(W*y+x, frameId)
+(devicePrograms.cu:631), so splitting the frame-id range across ranks reproduces the
+single-GPU image exactly up to fp32 summation order.  The only exchange is one sum
+reduce of the W*H*3 fp32 accumulator to rank 0 (RCCL over xGMI on the GPU box; any
+torch.distributed backend works, gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+
+def frame_range(step: int, rank: int, world: int, spp: int, base: int = 1) -> tuple[int, int]:
+    """Weak scaling (bench.py): each rank renders `spp` frames per step; ranges are
+    disjoint over (step, rank) and contiguous in step-major, rank-minor order."""
+    return base + (step * world + rank) * spp, spp
+
+
+def split_frames(total_spp: int, rank: int, world: int, base: int = 1) -> tuple[int, int]:
+    """Strong scaling (BASELINE config 4): frame ids base .. base+total_spp-1 split into
+    `world` contiguous blocks (GPU g renders base + g*spp/N .. base + (g+1)*spp/N - 1)."""
+    per, extra = divmod(total_spp, world)
+    first = base + rank * per + min(rank, extra)
+    return first, per + (1 if rank < extra else 0)
+
+
+def reduce_accumulator(tensor, dist, dst: int = 0) -> None:
+    """Sum every rank's accumulator into rank `dst` (one collective per image)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.reduce(tensor, dst=dst, op=dist.ReduceOp.SUM)

@@ -76,6 +76,9 @@ def load() -> C.CDLL:
     lib.orc_bsdf_eval.argtypes = [C.c_int32, _UP, _FP, C.c_float, _FP, _FP, _FP]
     lib.orc_bsdf_pdf.restype = C.c_float
     lib.orc_bsdf_pdf.argtypes = [C.c_int32, C.c_float, _FP, _FP]
+    lib.orc_cos_theta.restype = C.c_float
+    lib.orc_cos_theta.argtypes = [_FP]
+    lib.orc_furnace.argtypes = [C.c_int32, _UP, _FP, C.c_float, _FP, C.c_int32, _FP]
     lib.orc_camera_from_blender.argtypes = [_FP, _FP, C.c_float, C.c_int32, C.c_int32, _FP, _FP, _FP]
     lib.orc_camera_ray.argtypes = [C.POINTER(orc_launch), C.c_int32, C.c_int32, _FP, _FP]
     lib.orc_scene_create.restype = C.c_void_p
@@ -126,6 +129,18 @@ def bsdf_eval(model: str, seed: int, albedo, roughness: float, wo, wi):
     s = C.c_uint32(seed & 0xFFFFFFFF)
     out = np.zeros(3, np.float32)
     load().orc_bsdf_eval(BSDF[model], C.byref(s), fp(_f(albedo)), float(roughness), fp(_f(wo)), fp(_f(wi)), fp(out))
+    return out, int(s.value)
+
+
+def cos_theta(w) -> float:
+    return float(load().orc_cos_theta(fp(_f(w))))
+
+
+def furnace(model: str, seed: int, albedo, roughness: float, wo, n: int):
+    """mean of f*|cos|/pdf over n samples (UnitTests/SpherGeom_Test.cpp:28-252); returns (mean, seed')."""
+    s = C.c_uint32(seed & 0xFFFFFFFF)
+    out = np.zeros(3, np.float32)
+    load().orc_furnace(BSDF[model], C.byref(s), fp(_f(albedo)), float(roughness), fp(_f(wo)), int(n), fp(out))
     return out, int(s.value)
 
 

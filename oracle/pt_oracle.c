@@ -701,6 +701,25 @@ void orc_bsdf_eval(int32_t model, uint32_t* seed, const float albedo[3], float r
     }
     out[0] = r.x; out[1] = r.y; out[2] = r.z;
 }
+/* UnitTests/SpherGeom_Test.cpp:17-22 (PBRT::SpherGeom::CosTheta, SphericalGeometry.h:8) */
+float orc_cos_theta(const float w[3]) { return w[2]; }
+
+/* Furnace loop of UnitTests/SpherGeom_Test.cpp:28-252: mean over n samples of
+ * f*|cos|/pdf (AbsDot(dir, (0,0,1))) for one wo, one shared seed (advanced in place). */
+void orc_furnace(int32_t model, uint32_t* seed, const float albedo[3], float roughness, const float wo[3],
+                 int32_t n, float out[3]) {
+    v3 a = mk(albedo[0], albedo[1], albedo[2]), w = mk(wo[0], wo[1], wo[2]);
+    v3 acc = mk(0, 0, 0);
+    for (int32_t j = 0; j < n; ++j) {
+        bsample b;
+        memset(&b, 0, sizeof b);
+        int ok = (model == ORC_BSDF_CONDUCTOR) ? conductor_sample(seed, a, roughness, w, &b)
+                                                : layered_sample(seed, a, roughness, w, &b);
+        if (ok) acc = add(acc, divs(muls(b.color, absdot(b.dir, ZAXIS)), b.pdf));
+    }
+    out[0] = acc.x / (float)n; out[1] = acc.y / (float)n; out[2] = acc.z / (float)n;
+}
+
 float orc_bsdf_pdf(int32_t model, float roughness, const float wo[3], const float wi[3]) {
     v3 o = mk(wo[0], wo[1], wo[2]), i = mk(wi[0], wi[1], wi[2]);
     if (model == ORC_BSDF_LAMBERT) return lambert_pdf(o, i, 1);

@@ -69,6 +69,10 @@ int32_t orc_bsdf_sample(int32_t model, uint32_t* seed, const float albedo[3], fl
 void orc_bsdf_eval(int32_t model, uint32_t* seed, const float albedo[3], float roughness,
                    const float wo[3], const float wi[3], float out[3]);
 float orc_bsdf_pdf(int32_t model, float roughness, const float wo[3], const float wi[3]);
+/* reference unit-test known answers (UnitTests/SpherGeom_Test.cpp) */
+float orc_cos_theta(const float w[3]);
+void orc_furnace(int32_t model, uint32_t* seed, const float albedo[3], float roughness, const float wo[3],
+                 int32_t n, float out[3]);
 
 /* --- camera (Camera.cpp:37-70, GlmHelperMethods.cpp:4-10, OptixRenderer.cpp:662-668) --- */
 void orc_camera_from_blender(const float blender_pos[3], const float blender_rot_deg[3],

@@ -1,0 +1,193 @@
+"""CPU oracle checks (no GPU).
+
+Pins, strongest first:
+  1. independent pure-Python restatements of TEA-16 / LCG (random.h:34-69 constants);
+  2. the reference's own unit-test known answers (UnitTests/SpherGeom_Test.cpp): the
+     CosTheta KAT (:17-22) and the furnace bounds max(mean f|cos|/pdf) < 1.01 for
+     Conductor and GlossyDiffuse at roughness 0 / 0.5 / 1 (:28-252);
+  3. physical sanity (reciprocity-free properties the reference BSDFs must satisfy);
+  4. golden fixtures (tests/golden/golden.npz, made by tests/golden/make_golden.py) that
+     freeze the oracle bit-for-bit.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+GOLDEN = Path(__file__).resolve().parent / "golden" / "golden.npz"
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(GOLDEN)
+
+
+def py_tea16(v0, v1):
+    s0 = 0
+    M = 0xFFFFFFFF
+    for _ in range(16):
+        s0 = (s0 + 0x9E3779B9) & M
+        v0 = (v0 + ((((v1 << 4) & M) + 0xA341316C) ^ ((v1 + s0) & M) ^ ((v1 >> 5) + 0xC8013EA4))) & M
+        v1 = (v1 + ((((v0 << 4) & M) + 0xAD90777D) ^ ((v0 + s0) & M) ^ ((v0 >> 5) + 0x7E95761E))) & M
+    return v0
+
+
+def py_rnd(seed, n):
+    out = []
+    for _ in range(n):
+        seed = (1664525 * seed + 1013904223) & 0xFFFFFFFF
+        out.append(np.float32(seed & 0xFFFFFF) / np.float32(16777216.0))
+    return np.array(out, np.float32), seed
+
+
+def test_tea_matches_independent_restatement(oracle_lib, golden):
+    for (a, b), want in zip(golden["tea_in"], golden["tea_out"]):
+        assert oracle_lib.tea16(int(a), int(b)) == int(want) == py_tea16(int(a), int(b))
+
+
+def test_lcg_rnd_matches_independent_restatement(oracle_lib, golden):
+    for s, seq, fin in zip(golden["rnd_seeds"], golden["rnd_seq"], golden["rnd_final"]):
+        got, f = oracle_lib.rnd_seq(int(s), 16)
+        want, wf = py_rnd(int(s), 16)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(got, seq)
+        assert f == wf == int(fin)
+        assert np.all(got >= 0) and np.all(got < 1)
+
+
+def test_f2u_saturating_like_ptx_cvt_rzi_u32_f32(oracle_lib):
+    lib = oracle_lib.load()
+    assert lib.orc_f2u_sat(-5.5) == 0
+    assert lib.orc_f2u_sat(float("nan")) == 0
+    assert lib.orc_f2u_sat(3.99) == 3
+    assert lib.orc_f2u_sat(1e12) == 0xFFFFFFFF
+    assert lib.orc_f2u_sat(-0.0) == 0
+
+
+def test_reference_kat_cos_theta(oracle_lib):
+    # UnitTests/SpherGeom_Test.cpp:17-22: CosTheta((1,2,3)) == 3
+    assert oracle_lib.cos_theta([1.0, 2.0, 3.0]) == 3.0
+
+
+def _hemisphere_dirs(n, seed):
+    # SampleUniformHemisphere of SpherGeom_Test.cpp:300-305 over deterministic u
+    rng = np.random.default_rng(seed)
+    u = rng.uniform(size=(n, 2))
+    z = u[:, 0]
+    r = np.sqrt(np.maximum(0, 1 - z * z))
+    phi = 2 * 3.14159265359 * u[:, 1]
+    return np.stack([r * np.cos(phi), r * np.sin(phi), z], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("model", ["conductor", "layered"])
+@pytest.mark.parametrize("roughness", [0.0, 0.5, 1.0])
+def test_reference_furnace_bounds(oracle_lib, model, roughness):
+    """EnergyConservation_{Conductor,GlossyDiffuse}{0,05,1}R: albedo 1, seed literal
+    15615615665 (truncates to 2730713777), 10 wo, 16384 samples, max(mean) < 1.01."""
+    seed = 15615615665 & 0xFFFFFFFF
+    assert seed == 2730713777
+    wos = _hemisphere_dirs(10, 1)
+    wos[:, 2] = np.maximum(wos[:, 2], 1e-3)
+    for wo in wos:
+        mean, seed = oracle_lib.furnace(model, seed, [1.0, 1.0, 1.0], roughness, wo, 16384)
+        assert np.max(mean) < 1.01, (model, roughness, wo, mean)
+        assert np.all(mean >= 0)
+    # a smooth conductor of albedo 1 reflects (almost) everything
+    if model == "conductor" and roughness == 0.0:
+        assert np.min(mean) > 0.99
+
+
+def test_bsdf_sanity(oracle_lib):
+    alb = [0.5, 0.5, 0.5]
+    wo = np.array([0.3, 0.2, 0.932], np.float32)
+    wi = np.array([-0.4, 0.1, 0.911], np.float32)
+    lam, _ = oracle_lib.bsdf_eval("lambert", 1, alb, 0.5, wo, wi)
+    np.testing.assert_allclose(lam, np.float32(0.5) * np.float32(0.31830988618379067154), rtol=0)
+    below = wi * np.array([1, 1, -1], np.float32)
+    assert np.all(oracle_lib.bsdf_eval("lambert", 1, alb, 0.5, wo, below)[0] == 0)
+    # smooth conductor / dielectric have f == 0 (quirk 10, Conductor.h:102-103, Dielectric.h:100-101)
+    assert np.all(oracle_lib.bsdf_eval("conductor", 1, alb, 0.0, wo, wi)[0] == 0)
+    assert np.all(oracle_lib.bsdf_eval("dielectric", 1, alb, 0.0, wo, wi)[0] == 0)
+    # smooth dielectric draws exactly one random number (uc, Dielectric.h:149)
+    ok, out, s2 = oracle_lib.bsdf_sample("dielectric", 123, alb, 0.0, wo)
+    _, s1 = oracle_lib.rnd_seq(123, 1)
+    assert ok and s2 == s1
+    # Lambert sample always lands in z >= 0 even for wo below (quirk 9)
+    ok, out, _ = oracle_lib.bsdf_sample("lambert", 9, alb, 0.5, -wo)
+    assert ok and out[6] >= 0
+
+
+def test_golden_bsdf_tuples(oracle_lib, golden):
+    models = ["lambert", "conductor", "dielectric", "layered"]
+    alb = golden["bsdf_albedo"]
+    for row, ws, we in zip(golden["bsdf_in"], golden["bsdf_sample"], golden["bsdf_eval"]):
+        m, r, seed = models[int(row[0])], float(np.float32(row[1])), int(row[2])
+        wo, wi = row[3:6].astype(np.float32), row[6:9].astype(np.float32)
+        ok, out, s2 = oracle_lib.bsdf_sample(m, seed, alb, r, wo)
+        assert float(ok) == ws[0] and s2 == int(ws[9])
+        np.testing.assert_array_equal(out, ws[1:9].astype(np.float32))
+        ev, s3 = oracle_lib.bsdf_eval(m, seed, alb, r, wo, wi)
+        np.testing.assert_array_equal(ev, we[:3].astype(np.float32))
+        assert s3 == int(we[3])
+
+
+def test_golden_camera(oracle_lib, golden):
+    from optixpathtracer_amd import scenes
+
+    for row, ((pos, rot), (w, h)) in zip(golden["camera"], [(scenes.SCENE1_CAMERA, (1920, 1080)),
+                                                          (scenes.SCENE1_CAMERA, (256, 256)),
+                                                          (scenes.SCENE2_CAMERA, (1920, 1080))]):
+        p, iv, ip = oracle_lib.camera_from_blender(pos, rot, 40.0, w, h)
+        np.testing.assert_array_equal(np.concatenate([p, iv, ip]), row)
+    # Scene1 camera: engine position (3.85382, 1, 0), looking along -x (Camera.cpp:37-49)
+    p, iv, _ = oracle_lib.camera_from_blender(*scenes.SCENE1_CAMERA, 40.0, 1920, 1080)
+    np.testing.assert_allclose(p, [3.85382, 1.0, 0.0], atol=1e-6)
+    np.testing.assert_allclose(-iv[8:11], [-1, 0, 0], atol=1e-6)  # -(view z axis) = forward
+
+
+def test_golden_tiny_images(oracle_lib, golden):
+    from optixpathtracer_amd import scenes
+
+    for name, want in zip(golden["tiny_variants"], golden["tiny_images"]):
+        sc = scenes.tiny_scene(str(name))
+        o = oracle_lib.OracleScene(sc)
+        lp = o.launch(32, 24, 4)
+        img, _ = o.render(lp, 1, 4, threads=4)
+        np.testing.assert_array_equal(img, want)
+        o.close()
+
+
+def test_render_is_thread_count_invariant(oracle_lib):
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("layered")
+    o = oracle_lib.OracleScene(sc)
+    lp = o.launch(24, 16, 3)
+    a, sa = o.render(lp, 3, 2, threads=1)
+    b, sb = o.render(lp, 3, 2, threads=7)
+    np.testing.assert_array_equal(a, b)
+    assert sa == sb
+    # accumulation in two chunks == one pass (sequential fp32 adds in frame order)
+    c, _ = o.render(lp, 3, 1, threads=3)
+    c, _ = o.render(lp, 4, 1, sum_rgb=c, threads=3)
+    np.testing.assert_array_equal(a, c)
+    o.close()
+
+
+def test_trace_tie_break_is_structure_independent(oracle_lib):
+    """Closest hit is ordered by (t, global triangle index): duplicate coplanar triangles
+    resolve to the lower index regardless of BVH order."""
+    from optixpathtracer_amd import scenes
+
+    v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
+    m1 = scenes.Mesh(vertices=v, indices=np.array([[0, 1, 2]], np.int32), normals=np.tile([0, 0, 1], (3, 1)).astype(np.float32))
+    m2 = scenes.Mesh(vertices=v.copy(), indices=np.array([[0, 1, 2]], np.int32), normals=m1.normals.copy())
+    sc = scenes.Scene(meshes=[m1, m2], lights=np.zeros((0, 6), np.float32), camera_blender_pos=(0, 0, 0),
+                      camera_blender_rot=(0, 0, 0))
+    o = oracle_lib.OracleScene(sc)
+    rays = np.array([[0.25, 0.25, 1, 0, 0, -1, 0, 100], [0.25, 0.25, -1, 0, 0, 1, 0, 100]], np.float32)
+    prim, t, u, v_, back = o.trace(rays)
+    assert list(prim) == [0, 0]
+    assert list(back) == [0, 1]
+    np.testing.assert_allclose(t, [1, 1])
+    o.close()
