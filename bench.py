@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024, help="samples per pixel per GPU per step")
     ap.add_argument("--depth", type=int, default=8)
-    ap.add_argument("--kernel", type=int, default=0, help="0 = megakernel, 1 = wavefront")
+    ap.add_argument("--kernel", type=int, default=2, help="0 = megakernel, 1 = wavefront, 2 = auto")
     ap.add_argument("--frames-per-launch", type=int, default=8)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -198,7 +198,7 @@ def main():
                 "spp_per_gpu_per_step": args.spp,
                 "max_depth": args.depth,
                 "material_mode": "lambert" if scene.material_mode == 1 else str(scene.material_mode),
-                "kernel": "megakernel" if args.kernel == 0 else "wavefront",
+                "kernel": {0: "megakernel", 1: "wavefront", 2: "auto"}[args.kernel],
                 "frames_per_launch": args.frames_per_launch,
                 "parallelism": f"spp-shard x{world}",
                 "lbvh_build_ms": round(bvh_ms, 3),

@@ -34,7 +34,8 @@ extern "C" {
 
 /* Render-kernel variants (all produce the same image). */
 #define PT_KERNEL_MEGA 0      /* one thread per pixel, frames looped in registers */
-#define PT_KERNEL_WAVEFRONT 1 /* persistent wavefront: SoA ray/hit queues, wave compaction */
+#define PT_KERNEL_WAVEFRONT 1 /* wavefront: per-bounce kernels over SoA ray/hit queues, wave compaction */
+#define PT_KERNEL_AUTO 2      /* the faster of the two per material mode (measured) */
 
 /* Mesh: ModelLoading/Mesh.h:9-45 (vertecies, normal, texCoord, index, ModelMatrix, albedo,
  * metallic, roughness, texture ids).  Borrowed only during pt_create (deep copy). */
@@ -90,11 +91,16 @@ typedef struct pt_stats {
     uint64_t render_calls;    /* pt_render / pt_render_frames calls since pt_stats_reset */
     uint64_t kernel_launches; /* render-kernel launches since pt_stats_reset; each one is
                                  bracketed by its own HIP event pair on the library stream */
-    double bvh_build_ms;      /* LBVH build device time (pt_create) */
-    int32_t bvh_nodes;        /* internal nodes */
+    double bvh_build_ms;      /* LBVH build + BVH4 collapse device time (pt_create) */
+    int32_t bvh_nodes;        /* BVH4 inner nodes */
     int32_t triangles;
     int32_t frames_per_launch;
-    int32_t reserved;
+    int32_t bvh_depth;        /* BVH4 levels */
+    /* traversal counters, only counted while pt_set_traversal_stats(r, 1) */
+    uint64_t nodes_visited;
+    uint64_t tri_tests;
+    uint64_t rays;
+    uint64_t stack_overflows;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -119,6 +125,8 @@ int pt_set_material_mode(pt_renderer* r, int32_t material_mode);
 int pt_set_kernel(pt_renderer* r, int32_t kernel);
 /* frames (spp) rendered per kernel launch by pt_render_frames (default 8). */
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames);
+/* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */
+int pt_set_traversal_stats(pt_renderer* r, int32_t enable);
 
 /* OptixRenderer::Render(glm::vec3 h_pixels[]) — OptixRenderer.cpp:617-647: frame.id++,
  * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before

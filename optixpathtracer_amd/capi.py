@@ -14,7 +14,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libptamd.so"
 
 PT_MAT_DEFAULT, PT_MAT_LAMBERT, PT_MAT_CONDUCTOR, PT_MAT_DIELECTRIC, PT_MAT_LAYERED = range(5)
-PT_KERNEL_MEGA, PT_KERNEL_WAVEFRONT = 0, 1
+PT_KERNEL_MEGA, PT_KERNEL_WAVEFRONT, PT_KERNEL_AUTO = 0, 1, 2
 
 MATERIAL_MODES = {
     "default": PT_MAT_DEFAULT,
@@ -85,7 +85,11 @@ class pt_stats(C.Structure):
         ("bvh_nodes", C.c_int32),
         ("triangles", C.c_int32),
         ("frames_per_launch", C.c_int32),
-        ("reserved", C.c_int32),
+        ("bvh_depth", C.c_int32),
+        ("nodes_visited", C.c_uint64),
+        ("tri_tests", C.c_uint64),
+        ("rays", C.c_uint64),
+        ("stack_overflows", C.c_uint64),
     ]
 
 
@@ -104,6 +108,7 @@ SIGNATURES = {
     "pt_set_material_mode": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel": (C.c_int, [_R, C.c_int32]),
     "pt_set_frames_per_launch": (C.c_int, [_R, C.c_int32]),
+    "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),
     "pt_accum_clear": (C.c_int, [_R]),
     "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),

@@ -1,16 +1,23 @@
-// pt_build.hip — LBVH construction on gfx950 (replaces optixAccelBuild + compaction,
+// pt_build.hip — BVH construction on gfx950 (replaces optixAccelBuild + compaction,
 // Renderer/OptiX/OptixRenderer.cpp:306-456 of Damo12320/OptixPathtracer).
 //
 //   1. k_morton   : per triangle AABB centroid -> 30-bit Morton key (10 bits/axis)
 //   2. radix sort : (key, triangle) pairs, hipCUB device radix sort
-//   3. k_gather   : triangles + normals into leaf order; level 0 of an AABB sparse table
+//   3. k_gather   : triangle records into leaf order (isect: v0,e1,e2; shade: v1,v2,normals);
+//                   level 0 of an AABB sparse table over the sorted leaves
 //   4. k_sparse   : sparse-table level l = union of two level l-1 boxes (log2 N launches)
-//   5. k_karras   : one thread per internal node (Karras 2012 split search); each child's
-//                   AABB = O(1) sparse-table range query over its sorted leaf range
-// No inter-workgroup hand-offs: every kernel reads only what earlier launches wrote, so
-// the build needs no atomics or agent-scope fences and is deterministic.  The sparse
-// table costs N*log2(N)*32 B (≈150 MB at 250k triangles) — trivial against 288 GB HBM.
+//   5. k_karras   : binary LBVH, one thread per internal node (Karras 2012 split search);
+//                   each node's AABB = O(1) sparse-table range query over its leaf range
+//   6. k_collapse : top-down, one launch per BVH4 level: each BVH4 node greedily opens its
+//                   largest-area binary child until it has 4 children; a binary subtree of
+//                   <= kLeafMax triangles (a contiguous leaf range) becomes a BVH4 leaf.
+// Every kernel reads only what earlier launches wrote (no intra-launch hand-offs), so the
+// build needs no agent-scope fences; node numbering depends on atomic order but the
+// traversal result does not (closest hit is ordered by (t, triangle index)).  The sparse
+// table costs N*log2(N)*32 B (~150 MB at 250k triangles) — trivial against 288 GB HBM.
 #include <hipcub/hipcub.hpp>
+
+#include <vector>
 
 #include "pt_internal.h"
 
@@ -51,18 +58,22 @@ __global__ void k_morton(const float4* tri, int n, float3 cmin, float3 cinv, uin
     vals[i] = (uint32_t)i;
 }
 
-// leaf order gather + sparse-table level 0 (box = {lo.xyz,0},{hi.xyz,0})
-__global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const uint32_t* order, int n, float4* tri,
-                         float4* nrm, float4* st0) {
+// Leaf-order gather.  isect: v0|orig, (v1-v0)|material, (v2-v0)|0 — the edge subtraction
+// is the same single fp32 op the oracle performs, so the hit arithmetic stays identical.
+__global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const uint32_t* order, int n,
+                         float4* isect, float4* shade, float4* st0) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     int i = (int)order[k];
-    tri[3 * k] = tri_orig[3 * i];
-    tri[3 * k + 1] = tri_orig[3 * i + 1];
-    tri[3 * k + 2] = tri_orig[3 * i + 2];
-    nrm[3 * k] = nrm_orig[3 * i];
-    nrm[3 * k + 1] = nrm_orig[3 * i + 1];
-    nrm[3 * k + 2] = nrm_orig[3 * i + 2];
+    const float4 a = tri_orig[3 * i], b = tri_orig[3 * i + 1], c = tri_orig[3 * i + 2];
+    const float4 na = nrm_orig[3 * i], nb = nrm_orig[3 * i + 1], nc = nrm_orig[3 * i + 2];
+    isect[3 * k] = a;
+    isect[3 * k + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w);
+    isect[3 * k + 2] = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.0f);
+    shade[4 * k] = make_float4(b.x, b.y, b.z, na.x);
+    shade[4 * k + 1] = make_float4(c.x, c.y, c.z, na.y);
+    shade[4 * k + 2] = make_float4(na.z, nb.x, nb.y, nb.z);
+    shade[4 * k + 3] = make_float4(nc.x, nc.y, nc.z, 0.0f);
     float lo[3], hi[3];
     tri_box(tri_orig, i, lo, hi);
     st0[2 * k] = make_float4(lo[0], lo[1], lo[2], 0.0f);
@@ -83,22 +94,15 @@ struct SparseTable {
     int n;
 };
 
-__device__ __forceinline__ void range_box(const SparseTable& st, int a, int b, float lo[3], float hi[3]) {
+__device__ __forceinline__ void range_box(const SparseTable& st, int a, int b, float4& lo, float4& hi) {
     int len = b - a + 1;
     int l = 31 - __clz(len);
     const float4* L = st.level[l];
     int c = b - (1 << l) + 1;
     float4 a0 = L[2 * a], a1 = L[2 * a + 1], b0 = L[2 * c], b1 = L[2 * c + 1];
-    lo[0] = fminf(a0.x, b0.x);
-    lo[1] = fminf(a0.y, b0.y);
-    lo[2] = fminf(a0.z, b0.z);
-    hi[0] = fmaxf(a1.x, b1.x);
-    hi[1] = fmaxf(a1.y, b1.y);
-    hi[2] = fmaxf(a1.z, b1.z);
+    lo = make_float4(fminf(a0.x, b0.x), fminf(a0.y, b0.y), fminf(a0.z, b0.z), 0.0f);
+    hi = make_float4(fmaxf(a1.x, b1.x), fmaxf(a1.y, b1.y), fmaxf(a1.z, b1.z), 0.0f);
 }
-
-// Conservative padding so the traversal's fma slab test never culls a true hit.
-__device__ __forceinline__ float pad_amount(float x) { return fabsf(x) * 9.5367431640625e-7f + 1e-6f; }
 
 __device__ __forceinline__ int delta(const uint32_t* keys, int n, int i, int j) {
     if (j < 0 || j >= n) return -1;
@@ -107,7 +111,8 @@ __device__ __forceinline__ int delta(const uint32_t* keys, int n, int i, int j) 
     return __clz(ki ^ kj);
 }
 
-__global__ void k_karras(const uint32_t* keys, int n, SparseTable st, BNode* nodes) {
+// Binary LBVH node i: child codes (>= 0 internal, < 0 leaf ~k), leaf range, AABB.
+__global__ void k_karras(const uint32_t* keys, int n, SparseTable st, int2* bchild, int2* brange, float4* bbox) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n - 1) return;
     int d = (delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -128,21 +133,113 @@ __global__ void k_karras(const uint32_t* keys, int n, SparseTable st, BNode* nod
     int first = min(i, j), last = max(i, j);
     int c0 = (first == gamma) ? ~gamma : gamma;
     int c1 = (last == gamma + 1) ? ~(gamma + 1) : (gamma + 1);
-    float lo0[3], hi0[3], lo1[3], hi1[3];
-    range_box(st, first, gamma, lo0, hi0);
-    range_box(st, gamma + 1, last, lo1, hi1);
-    for (int a = 0; a < 3; ++a) {
-        lo0[a] -= pad_amount(lo0[a]);
-        hi0[a] += pad_amount(hi0[a]);
-        lo1[a] -= pad_amount(lo1[a]);
-        hi1[a] += pad_amount(hi1[a]);
+    bchild[i] = make_int2(c0, c1);
+    brange[i] = make_int2(first, last);
+    float4 lo, hi;
+    range_box(st, first, last, lo, hi);
+    bbox[2 * i] = lo;
+    bbox[2 * i + 1] = hi;
+}
+
+struct BinTree {
+    const int2* child;
+    const int2* range;
+    const float4* box;  // internal node boxes (2 per node)
+    const float4* leafbox;  // sparse table level 0 (2 per leaf)
+};
+
+__device__ __forceinline__ void code_box(const BinTree& B, int code, float4& lo, float4& hi) {
+    if (code >= 0) {
+        lo = B.box[2 * code];
+        hi = B.box[2 * code + 1];
+    } else {
+        lo = B.leafbox[2 * ~code];
+        hi = B.leafbox[2 * ~code + 1];
     }
-    BNode nd;
-    nd.a = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
-    nd.b = make_float4(lo1[0], hi1[0], lo1[1], hi1[1]);
-    nd.c = make_float4(lo0[2], hi0[2], lo1[2], hi1[2]);
-    nd.d = make_int4(c0, c1, 0, 0);
-    nodes[i] = nd;
+}
+__device__ __forceinline__ int code_count(const BinTree& B, int code) {
+    if (code < 0) return 1;
+    int2 r = B.range[code];
+    return r.y - r.x + 1;
+}
+__device__ __forceinline__ int code_first(const BinTree& B, int code) { return code < 0 ? ~code : B.range[code].x; }
+__device__ __forceinline__ float half_area(float4 lo, float4 hi) {
+    float x = hi.x - lo.x, y = hi.y - lo.y, z = hi.z - lo.z;
+    return x * y + y * z + z * x;
+}
+// Conservative padding so the traversal's fma slab test never culls a true hit.
+__device__ __forceinline__ float pad_amount(float x) { return fabsf(x) * 9.5367431640625e-7f + 1e-6f; }
+
+// One BVH4 node per work item: (binary code, BVH4 slot).
+__global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, int* counter, int2* next,
+                           int* nnext) {
+    int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwork) return;
+    const int2 item = work[w];
+    int c[4];
+    int n;
+    if (item.x >= 0) {
+        int2 ch = B.child[item.x];
+        c[0] = ch.x;
+        c[1] = ch.y;
+        n = 2;
+    } else {  // degenerate scene: the root is a single leaf
+        c[0] = item.x;
+        n = 1;
+    }
+    while (n < 4) {  // open the largest-area child that cannot be a leaf
+        int best = -1;
+        float ba = -1.0f;
+        for (int k = 0; k < n; ++k) {
+            if (c[k] < 0 || code_count(B, c[k]) <= kLeafMax) continue;
+            float4 lo, hi;
+            code_box(B, c[k], lo, hi);
+            float a = half_area(lo, hi);
+            if (a > ba) {
+                ba = a;
+                best = k;
+            }
+        }
+        if (best < 0) break;
+        int2 ch = B.child[c[best]];
+        c[best] = ch.x;
+        c[n++] = ch.y;
+    }
+    float lo[3][4], hi[3][4];
+    int cc[4];
+    for (int k = 0; k < 4; ++k) {
+        if (k >= n) {
+            cc[k] = kEmptyChild;
+            for (int a = 0; a < 3; ++a) lo[a][k] = hi[a][k] = 0.0f;
+            continue;
+        }
+        float4 l4, h4;
+        code_box(B, c[k], l4, h4);
+        float l[3] = {l4.x, l4.y, l4.z}, h[3] = {h4.x, h4.y, h4.z};
+        for (int a = 0; a < 3; ++a) {
+            lo[a][k] = l[a] - pad_amount(l[a]);
+            hi[a][k] = h[a] + pad_amount(h[a]);
+        }
+        int cnt = code_count(B, c[k]);
+        if (cnt <= kLeafMax) {
+            cc[k] = ~((code_first(B, c[k]) << 3) | (cnt - 1));
+        } else {
+            int slot = atomicAdd(counter, 1);
+            cc[k] = slot;
+            int q = atomicAdd(nnext, 1);
+            next[q] = make_int2(c[k], slot);
+        }
+    }
+    BNode4 nd;
+    nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    nd.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    nd.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    nd.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    nd.child = make_int4(cc[0], cc[1], cc[2], cc[3]);
+    nd.pad = make_int4(0, 0, 0, 0);
+    out[item.y] = nd;
 }
 
 inline unsigned grid_for(int n, int b) { return (unsigned)((n + b - 1) / b); }
@@ -162,13 +259,21 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     const int n = in.n;
     hipError_t err = hipSuccess;
     uint32_t *keys = nullptr, *vals = nullptr, *keys2 = nullptr, *vals2 = nullptr;
-    float4* st = nullptr;
+    float4 *st = nullptr, *bbox = nullptr;
+    int2 *bchild = nullptr, *brange = nullptr, *work = nullptr, *work2 = nullptr;
+    int* cnt = nullptr;  // [0] node counter, [1] next-level work count
     void* temp = nullptr;
     size_t temp_bytes = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int levels = 1;
     SparseTable table{};
+    BinTree B{};
+    int h_cnt[2] = {1, 0};
+    int nwork = 1, depth = 0;
+    const int nbin = n > 1 ? n - 1 : 1;
     if (ms) *ms = 0.0f;
+    out.n_nodes = 0;
+    out.depth = 0;
     if (n <= 0) return hipSuccess;
     while ((1 << levels) <= n) ++levels;  // levels 0..levels-1 with 2^l <= n
     PT_TRY(hipEventCreate(&e0));
@@ -178,6 +283,12 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     PT_TRY(hipMalloc(&keys2, sizeof(uint32_t) * n));
     PT_TRY(hipMalloc(&vals2, sizeof(uint32_t) * n));
     PT_TRY(hipMalloc(&st, sizeof(float4) * 2 * (size_t)n * (size_t)levels));
+    PT_TRY(hipMalloc(&bchild, sizeof(int2) * nbin));
+    PT_TRY(hipMalloc(&brange, sizeof(int2) * nbin));
+    PT_TRY(hipMalloc(&bbox, sizeof(float4) * 2 * nbin));
+    PT_TRY(hipMalloc(&work, sizeof(int2) * n));
+    PT_TRY(hipMalloc(&work2, sizeof(int2) * n));
+    PT_TRY(hipMalloc(&cnt, sizeof(int) * 2));
     PT_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, n, 0, 30, stream));
     PT_TRY(hipMalloc(&temp, temp_bytes > 0 ? temp_bytes : 16));
     PT_TRY(hipEventRecord(e0, stream));
@@ -191,7 +302,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
         PT_TRY(hipGetLastError());
         PT_TRY(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, n, 0, 30, stream));
         hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig, vals2,
-                           n, out.tri, out.nrm, st);
+                           n, out.isect, out.shade, st);
         PT_TRY(hipGetLastError());
         table.n = n;
         table.level[0] = st;
@@ -205,21 +316,41 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             table.level[l] = cur;
         }
         if (n > 1) {
-            hipLaunchKernelGGL(k_karras, dim3(grid_for(n - 1, 256)), dim3(256), 0, stream, keys2, n, table,
-                               out.nodes);
+            hipLaunchKernelGGL(k_karras, dim3(grid_for(n - 1, 256)), dim3(256), 0, stream, keys2, n, table, bchild,
+                               brange, bbox);
             PT_TRY(hipGetLastError());
+        }
+        B.child = bchild;
+        B.range = brange;
+        B.box = bbox;
+        B.leafbox = st;
+        // root work item: binary node 0 (or the single leaf ~0) -> BVH4 slot 0
+        int2 root = make_int2(n > 1 ? 0 : ~0, 0);
+        PT_TRY(hipMemcpyAsync(work, &root, sizeof(int2), hipMemcpyHostToDevice, stream));
+        PT_TRY(hipMemcpyAsync(cnt, h_cnt, sizeof(int) * 2, hipMemcpyHostToDevice, stream));
+        while (nwork > 0) {
+            PT_TRY(hipMemsetAsync(cnt + 1, 0, sizeof(int), stream));
+            hipLaunchKernelGGL(k_collapse, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, work, nwork,
+                               out.nodes, cnt, work2, cnt + 1);
+            PT_TRY(hipGetLastError());
+            PT_TRY(hipMemcpyAsync(h_cnt, cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
+            PT_TRY(hipStreamSynchronize(stream));
+            nwork = h_cnt[1];
+            ++depth;
+            int2* t = work;
+            work = work2;
+            work2 = t;
         }
     }
     PT_TRY(hipEventRecord(e1, stream));
     PT_TRY(hipEventSynchronize(e1));
     if (ms) PT_TRY(hipEventElapsedTime(ms, e0, e1));
+    out.n_nodes = h_cnt[0];
+    out.depth = depth;
 done:
-    if (keys) (void)hipFree(keys);
-    if (vals) (void)hipFree(vals);
-    if (keys2) (void)hipFree(keys2);
-    if (vals2) (void)hipFree(vals2);
-    if (st) (void)hipFree(st);
-    if (temp) (void)hipFree(temp);
+    for (void* p : {(void*)keys, (void*)vals, (void*)keys2, (void*)vals2, (void*)st, (void*)bchild, (void*)brange,
+                    (void*)bbox, (void*)work, (void*)work2, (void*)cnt, temp})
+        if (p) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     return err;

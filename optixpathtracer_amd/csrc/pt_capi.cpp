@@ -46,9 +46,12 @@ struct pt_renderer {
     int device = 0;
     hipStream_t stream = nullptr;
     // scene
-    BNode* d_nodes = nullptr;
-    float4* d_tri = nullptr;
-    float4* d_nrm = nullptr;
+    BNode4* d_nodes = nullptr;
+    float4* d_isect = nullptr;
+    float4* d_shade = nullptr;
+    int bvh_nodes = 0, bvh_depth = 0;
+    bool trav_stats = false;
+    WFState wf;
     float4* d_mats = nullptr;
     int ntri = 0;
     int nmesh = 0;
@@ -83,8 +86,8 @@ struct pt_renderer {
     DevScene scene() const {
         DevScene S;
         S.nodes = d_nodes;
-        S.tri = d_tri;
-        S.nrm = d_nrm;
+        S.isect = d_isect;
+        S.shade = d_shade;
         S.mats = d_mats;
         S.ntri = ntri;
         return S;
@@ -150,6 +153,35 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
     r->pending = true;
+    // AUTO: the megakernel wins where the BRDF eval has no RNG side effects (Lambert,
+    // Conductor, Dielectric: short, uniform shading); the wavefront wins on Default/Layered,
+    // whose random-walk BSDF would otherwise stall the traversal waves.
+    int kernel = r->kernel;
+    if (kernel == PT_KERNEL_AUTO)
+        kernel = (r->material_mode == PT_MAT_DEFAULT || r->material_mode == PT_MAT_LAYERED) ? PT_KERNEL_WAVEFRONT
+                                                                                            : PT_KERNEL_MEGA;
+    if (kernel == PT_KERNEL_WAVEFRONT) {
+        const int P = r->width * r->height;
+        if (r->wf.paths != P || r->wf.max_bounces < r->max_bounces) {
+            PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+            wavefront_free(r->wf);
+            PT_HIP(wavefront_alloc(r->wf, P, std::max(1, r->max_bounces)), "wavefront_alloc");
+        }
+        int dev_cus = 256;
+        (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, r->device);
+        for (uint32_t f = 0; f < n; ++f) {  // one event pair per frame (the frame's kernel chain)
+            DevLaunch L = make_launch(r, accum, first + f, 1);
+            hipEvent_t a, b;
+            rc = next_event_pair(r, &a, &b);
+            if (rc) return rc;
+            PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
+            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, dev_cus,
+                                          r->stream),
+                   "wavefront launch");
+            PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
+        }
+        done = n;
+    }
     while (done < n) {
         uint32_t k = std::min(chunk, n - done);
         DevLaunch L = make_launch(r, accum, first + done, k);
@@ -157,7 +189,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
         rc = next_event_pair(r, &a, &b);
         if (rc) return rc;
         PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
-        PT_HIP(launch_render(r->kernel, r->material_mode, S, L, r->stream), "render launch");
+        PT_HIP(launch_render(kernel, r->material_mode, r->trav_stats, S, L, r->stream), "render launch");
         PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
         done += k;
     }
@@ -183,7 +215,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     pt_options opt{};
     if (options) opt = *options;
     if (!valid_mode(opt.material_mode)) return fail(PT_ERR_INVALID, "pt_create: invalid material_mode");
-    if (opt.kernel != PT_KERNEL_MEGA && opt.kernel != PT_KERNEL_WAVEFRONT)
+    if (opt.kernel != PT_KERNEL_MEGA && opt.kernel != PT_KERNEL_WAVEFRONT && opt.kernel != PT_KERNEL_AUTO)
         return fail(PT_ERR_INVALID, "pt_create: invalid kernel");
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
@@ -264,16 +296,16 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         if (e__ != hipSuccess) return cleanup_fail(hip_fail(e__, where)); \
     } while (0)
     PT_HIPC(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking), "hipStreamCreate");
-    PT_HIPC(hipMalloc(&r->d_counters, 4 * sizeof(unsigned long long)), "hipMalloc counters");
-    PT_HIPC(hipMemsetAsync(r->d_counters, 0, 4 * sizeof(unsigned long long), r->stream), "hipMemset");
+    PT_HIPC(hipMalloc(&r->d_counters, 8 * sizeof(unsigned long long)), "hipMalloc counters");
+    PT_HIPC(hipMemsetAsync(r->d_counters, 0, 8 * sizeof(unsigned long long), r->stream), "hipMemset");
     PT_HIPC(hipMalloc(&r->d_mats, sizeof(float4) * mats.size()), "hipMalloc mats");
     PT_HIPC(hipMemcpyAsync(r->d_mats, mats.data(), sizeof(float4) * mats.size(), hipMemcpyHostToDevice, r->stream),
             "upload mats");
     if (ntri > 0) {
         float4 *d_tri_orig = nullptr, *d_nrm_orig = nullptr;
-        PT_HIPC(hipMalloc(&r->d_tri, sizeof(float4) * 3 * ntri), "hipMalloc tri");
-        PT_HIPC(hipMalloc(&r->d_nrm, sizeof(float4) * 3 * ntri), "hipMalloc nrm");
-        PT_HIPC(hipMalloc(&r->d_nodes, sizeof(BNode) * std::max<size_t>(1, ntri - 1)), "hipMalloc nodes");
+        PT_HIPC(hipMalloc(&r->d_isect, sizeof(float4) * 3 * ntri), "hipMalloc isect");
+        PT_HIPC(hipMalloc(&r->d_shade, sizeof(float4) * 4 * ntri), "hipMalloc shade");
+        PT_HIPC(hipMalloc(&r->d_nodes, sizeof(BNode4) * std::max<size_t>(1, ntri)), "hipMalloc nodes");
         PT_HIPC(hipMalloc(&d_tri_orig, sizeof(float4) * 3 * ntri), "hipMalloc tri_orig");
         PT_HIPC(hipMalloc(&d_nrm_orig, sizeof(float4) * 3 * ntri), "hipMalloc nrm_orig");
         PT_HIPC(hipMemcpyAsync(d_tri_orig, tri.data(), sizeof(float4) * 3 * ntri, hipMemcpyHostToDevice, r->stream),
@@ -290,8 +322,8 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         }
         BuildOutput bo;
         bo.nodes = r->d_nodes;
-        bo.tri = r->d_tri;
-        bo.nrm = r->d_nrm;
+        bo.isect = r->d_isect;
+        bo.shade = r->d_shade;
         float ms = 0.0f;
         hipError_t be = lbvh_build(in, bo, r->stream, &ms);
         (void)hipStreamSynchronize(r->stream);
@@ -299,6 +331,8 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         (void)hipFree(d_nrm_orig);
         if (be != hipSuccess) return cleanup_fail(hip_fail(be, "lbvh_build"));
         r->bvh_ms = ms;
+        r->bvh_nodes = bo.n_nodes;
+        r->bvh_depth = bo.depth;
     }
     PT_HIPC(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
 #undef PT_HIPC
@@ -311,13 +345,14 @@ int pt_destroy(pt_renderer* r) {
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     (void)hipSetDevice(r->device);
     if (r->d_nodes) (void)hipFree(r->d_nodes);
-    if (r->d_tri) (void)hipFree(r->d_tri);
-    if (r->d_nrm) (void)hipFree(r->d_nrm);
+    if (r->d_isect) (void)hipFree(r->d_isect);
+    if (r->d_shade) (void)hipFree(r->d_shade);
     if (r->d_mats) (void)hipFree(r->d_mats);
     if (r->d_lights) (void)hipFree(r->d_lights);
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_counters) (void)hipFree(r->d_counters);
+    wavefront_free(r->wf);
     for (hipEvent_t e : r->ev_start) (void)hipEventDestroy(e);
     for (hipEvent_t e : r->ev_stop) (void)hipEventDestroy(e);
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -391,7 +426,7 @@ int pt_set_material_mode(pt_renderer* r, int32_t mode) {
 }
 
 int pt_set_kernel(pt_renderer* r, int32_t kernel) {
-    if (!r || (kernel != PT_KERNEL_MEGA && kernel != PT_KERNEL_WAVEFRONT))
+    if (!r || (kernel != PT_KERNEL_MEGA && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_AUTO))
         return fail(PT_ERR_INVALID, "pt_set_kernel: invalid");
     r->kernel = kernel;
     return PT_OK;
@@ -468,7 +503,7 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     if (!r || !out) return fail(PT_ERR_INVALID, "pt_get_stats: NULL");
     int rc = pt_synchronize(r);
     if (rc) return rc;
-    unsigned long long c[4];
+    unsigned long long c[8];
     PT_HIP(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost), "download counters");
     std::memset(out, 0, sizeof *out);
     out->segments = c[0];
@@ -479,7 +514,12 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->kernel_launches = r->launches;
     out->frames_per_launch = r->frames_per_launch;
     out->bvh_build_ms = r->bvh_ms;
-    out->bvh_nodes = r->ntri > 1 ? r->ntri - 1 : 0;
+    out->bvh_nodes = r->bvh_nodes;
+    out->bvh_depth = r->bvh_depth;
+    out->nodes_visited = c[1];
+    out->tri_tests = c[2];
+    out->rays = c[3];
+    out->stack_overflows = c[4];
     out->triangles = r->ntri;
     return PT_OK;
 }
@@ -488,7 +528,7 @@ int pt_stats_reset(pt_renderer* r) {
     if (!r) return fail(PT_ERR_INVALID, "pt_stats_reset: NULL");
     int rc = pt_synchronize(r);
     if (rc) return rc;
-    PT_HIP(hipMemset(r->d_counters, 0, 4 * sizeof(unsigned long long)), "hipMemset counters");
+    PT_HIP(hipMemset(r->d_counters, 0, 8 * sizeof(unsigned long long)), "hipMemset counters");
     r->samples = 0;
     r->last_ms = r->total_ms = 0.0;
     r->calls = 0;
@@ -612,3 +652,9 @@ int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* pr
 }
 
 }  // extern "C"
+
+extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_traversal_stats: NULL");
+    r->trav_stats = enable != 0;
+    return PT_OK;
+}

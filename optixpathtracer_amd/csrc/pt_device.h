@@ -1,31 +1,39 @@
-// pt_device.h — HBM layout of the scene, LBVH traversal and the path integrator for gfx950.
+// pt_device.h — HBM layout of the scene, BVH4 traversal and the path integrator for gfx950.
 //
 // Replaces, for the render path of Damo12320/OptixPathtracer:
 //   * optixTrace + the closed OptiX 7.3 traversal / triangle test (devicePrograms.cu:216-260)
 //   * __closesthit__radiance (devicePrograms.cu:343-514), __miss__radiance/__miss__shadow
 //     (:576-591), SamplePath (:625-664) and the camera of __raygen__renderFrame (:601-623).
 //
-// HBM layout (all arrays in LBVH leaf order, 16-byte aligned records):
-//   nodes  : BNode[N-1], 64 B — both children's AABBs + child links (leaf = ~triangle)
-//   tri    : float4[3N]       — v0.xyz|orig index, v1.xyz|material, v2.xyz|0 (world space)
-//   nrm    : float4[3N]       — world-space vertex normals of the triangle
-//   mats   : float4[2M]       — albedo.xyz|metallic, roughness|has_normals|0|0
+// HBM layout (triangle arrays in LBVH leaf order, 16-byte aligned records):
+//   nodes4 : BNode4[<N], 128 B — 4 child AABBs as SoA float4s + child links; one cache line
+//   isect  : float4[3N]         — v0.xyz|orig index, e1.xyz|material, e2.xyz|0  (e = v - v0,
+//                                  the same fp32 subtraction the oracle performs)
+//   shade  : float4[4N]         — v1.xyz|n0.x, v2.xyz|n0.y, n0.z n1.xyz, n2.xyz|0
+//   mats   : float4[2M]         — albedo.xyz|metallic, roughness|has_normals|0|0
+// Leaves reference up to kLeafMax consecutive triangles (an LBVH subtree is a contiguous
+// range of the Morton-sorted triangles, so no index indirection is needed).
 #pragma once
 #include "pt_bsdf.h"
 
 namespace pt {
 
-struct __align__(16) BNode {
-    float4 a;  // c0.lo.x c0.hi.x c0.lo.y c0.hi.y
-    float4 b;  // c1.lo.x c1.hi.x c1.lo.y c1.hi.y
-    float4 c;  // c0.lo.z c0.hi.z c1.lo.z c1.hi.z
-    int4 d;    // child0 child1 (>=0 internal node, <0 leaf = ~tri)
+constexpr int kLeafMax = 4;
+constexpr int kEmptyChild = (int)0x80000000;
+
+struct __align__(16) BNode4 {
+    float4 lox, hix, loy, hiy, loz, hiz;  // children 0..3
+    int4 child;                           // >=0 inner node; <0 leaf ~(first<<3 | count-1); kEmptyChild
+    int4 pad;
 };
 
+__device__ __forceinline__ int leaf_first(int c) { return (~c) >> 3; }
+__device__ __forceinline__ int leaf_count(int c) { return ((~c) & 7) + 1; }
+
 struct DevScene {
-    const BNode* nodes;
-    const float4* tri;
-    const float4* nrm;
+    const BNode4* nodes;
+    const float4* isect;
+    const float4* shade;
     const float4* mats;
     int ntri;
 };
@@ -45,7 +53,7 @@ struct DevLaunch {
     uint32_t frame_base;
     uint32_t n_frames;
     float* accum;                    // W*H*3 fp32 sum
-    unsigned long long* counters;    // [0] segments
+    unsigned long long* counters;    // [0] segments [1] nodes visited [2] triangle tests [3] rays
 };
 
 struct Hit {
@@ -55,14 +63,17 @@ struct Hit {
     bool back;
 };
 
+struct TravStats {
+    uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0;
+};
+
 // Moller-Trumbore; OptiX barycentric convention (u weights v1, v weights v2); closed
 // interval [tmin, tmax]; det < 0 <=> back face (ray along the CCW normal).  Same
-// arithmetic order as the oracle's tri_hit.
-__device__ __forceinline__ bool tri_intersect(const float4 a, const float4 b, const float4 c, f3 o, f3 d,
+// arithmetic order as the oracle's tri_hit (edges precomputed with the same subtraction).
+__device__ __forceinline__ bool tri_intersect(const float4 A, const float4 E1, const float4 E2, f3 o, f3 d,
                                               float tmin, float tmax, float& th, float& uh, float& vh,
                                               bool& back) {
-    f3 v0 = mk(a.x, a.y, a.z), v1 = mk(b.x, b.y, b.z), v2 = mk(c.x, c.y, c.z);
-    f3 e1 = v1 - v0, e2 = v2 - v0;
+    f3 v0 = mk(A.x, A.y, A.z), e1 = mk(E1.x, E1.y, E1.z), e2 = mk(E2.x, E2.y, E2.z);
     f3 p = cross(d, e2);
     float det = dot(e1, p);
     if (det == 0.0f) return false;
@@ -82,26 +93,6 @@ __device__ __forceinline__ bool tri_intersect(const float4 a, const float4 b, co
     return true;
 }
 
-// Slab test of both children; boxes are padded at build time so the fma form is conservative.
-__device__ __forceinline__ void box2(const BNode& n, f3 io, f3 inv, float tmin, float tmax, float& t0n,
-                                     float& t1n, bool& h0, bool& h1) {
-    const float k = 1.0000004f;
-    float ax = __fmaf_rn(n.a.x, inv.x, -io.x), bx = __fmaf_rn(n.a.y, inv.x, -io.x);
-    float ay = __fmaf_rn(n.a.z, inv.y, -io.y), by = __fmaf_rn(n.a.w, inv.y, -io.y);
-    float az = __fmaf_rn(n.c.x, inv.z, -io.z), bz = __fmaf_rn(n.c.y, inv.z, -io.z);
-    float n0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-    float f0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax)) * k;
-    float cx = __fmaf_rn(n.b.x, inv.x, -io.x), dx = __fmaf_rn(n.b.y, inv.x, -io.x);
-    float cy = __fmaf_rn(n.b.z, inv.y, -io.y), dy = __fmaf_rn(n.b.w, inv.y, -io.y);
-    float cz = __fmaf_rn(n.c.z, inv.z, -io.z), dz = __fmaf_rn(n.c.w, inv.z, -io.z);
-    float n1 = fmaxf(fmaxf(fminf(cx, dx), fminf(cy, dy)), fmaxf(fminf(cz, dz), tmin));
-    float f1 = fminf(fminf(fmaxf(cx, dx), fmaxf(cy, dy)), fminf(fmaxf(cz, dz), tmax)) * k;
-    t0n = n0;
-    t1n = n1;
-    h0 = n0 <= f0;
-    h1 = n1 <= f1;
-}
-
 // Reciprocal direction; zero components map to a huge finite value so the fma slab form
 // never produces 0*inf.
 __device__ __forceinline__ f3 safe_inv(f3 d) {
@@ -110,75 +101,111 @@ __device__ __forceinline__ f3 safe_inv(f3 d) {
               d.z != 0.0f ? 1.0f / d.z : copysignf(big, d.z));
 }
 
-constexpr int kStack = 64;
+// Slab test of one child (lane c of the SoA node); boxes are padded at build time so the
+// fma form is conservative; tfar is widened by 4 ulp-ish as PBRT's robust test does.
+__device__ __forceinline__ float slab(float lx, float hx, float ly, float hy, float lz, float hz, f3 inv, f3 io,
+                                      float tmin, float tmax, bool& hit) {
+    float ax = __fmaf_rn(lx, inv.x, -io.x), bx = __fmaf_rn(hx, inv.x, -io.x);
+    float ay = __fmaf_rn(ly, inv.y, -io.y), by = __fmaf_rn(hy, inv.y, -io.y);
+    float az = __fmaf_rn(lz, inv.z, -io.z), bz = __fmaf_rn(hz, inv.z, -io.z);
+    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax)) * 1.0000004f;
+    hit = tn <= tf;
+    return tn;
+}
+
+__device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
+    bool s = tb < ta;
+    float t0 = s ? tb : ta, t1 = s ? ta : tb;
+    int c0 = s ? cb : ca, c1 = s ? ca : cb;
+    ta = t0; tb = t1; ca = c0; cb = c1;
+}
+
+// LDS stack: entry s of thread tid at stk[s * kStackStride] with stk = base + tid, so the
+// 64 lanes of a wave always touch 64 consecutive dwords (conflict-free for any sp mix).
+constexpr int kStackDepth = 32;
+constexpr int kSpillDepth = 64;
 
 // Closest hit ordered by (t, original triangle index): independent of BVH shape.
-template <bool ANY>
-__device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h) {
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h,
+                                         int* __restrict__ stk, int stride, TravStats& ts) {
     h.tri = -1;
     h.orig = 0x7fffffff;
+    if (STATS) ts.rays++;
     if (S.ntri <= 0) return false;
-    if (S.ntri == 1) {
-        float t, u, v;
-        bool bk;
-        if (!tri_intersect(S.tri[0], S.tri[1], S.tri[2], o, d, tmin, tmax, t, u, v, bk)) return false;
-        h.t = t; h.u = u; h.v = v; h.back = bk; h.tri = 0;
-        h.orig = __float_as_int(S.tri[0].w);
-        return true;
-    }
-    f3 inv = safe_inv(d);
-    f3 io = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-    int stack[kStack];
-    int sp = 0;
-    int node = 0;
+    const f3 inv = safe_inv(d);
+    const f3 io = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
     float best = tmax;
+    int sp = 0;
+    int cur = 0;  // root (always an inner node)
+    // LDS holds the top kStackDepth entries; deeper ones (never seen on the benchmark
+    // scenes, see the overflow counter) go to a private spill array instead of being lost.
+    int spill[kSpillDepth];
+    auto push = [&](int c) {
+        if (sp < kStackDepth) stk[sp * stride] = c;
+        else if (sp < kStackDepth + kSpillDepth) spill[sp - kStackDepth] = c;
+        else { if (STATS) ts.overflow++; return; }
+        ++sp;
+    };
     while (true) {
-        const BNode n = S.nodes[node];
-        float t0, t1;
-        bool h0, h1;
-        box2(n, io, inv, tmin, best, t0, t1, h0, h1);
-        int c0 = n.d.x, c1 = n.d.y;
-        if (h0 && c0 < 0) {
-            int ti = ~c0;
-            float t, u, v;
-            bool bk;
-            float4 A = S.tri[3 * ti], B = S.tri[3 * ti + 1], C = S.tri[3 * ti + 2];
-            if (tri_intersect(A, B, C, o, d, tmin, best, t, u, v, bk)) {
-                int oi = __float_as_int(A.w);
-                if (ANY) { h.tri = ti; h.orig = oi; return true; }
-                if (t < best || oi < h.orig) {
-                    best = t; h.t = t; h.u = u; h.v = v; h.back = bk; h.tri = ti; h.orig = oi;
-                }
+        if (cur >= 0) {
+            if (STATS) ts.nodes++;
+            const BNode4& n = S.nodes[cur];
+            const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
+            const int4 ch = n.child;
+            bool h0, h1, h2, h3;
+            float t0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, inv, io, tmin, best, h0);
+            float t1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, inv, io, tmin, best, h1);
+            float t2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, inv, io, tmin, best, h2);
+            float t3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, inv, io, tmin, best, h3);
+            const float inf = __int_as_float(0x7f800000);
+            int c0 = (h0 && ch.x != kEmptyChild) ? ch.x : kEmptyChild;
+            int c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
+            int c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
+            int c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
+            t0 = c0 != kEmptyChild ? t0 : inf;
+            t1 = c1 != kEmptyChild ? t1 : inf;
+            t2 = c2 != kEmptyChild ? t2 : inf;
+            t3 = c3 != kEmptyChild ? t3 : inf;
+            // sort ascending (optimal 4-network); misses sink to the end with t = inf
+            cswap(t0, c0, t1, c1);
+            cswap(t2, c2, t3, c3);
+            cswap(t0, c0, t2, c2);
+            cswap(t1, c1, t3, c3);
+            cswap(t1, c1, t2, c2);
+            // push the farther hits (far first), continue with the nearest
+            if (c3 != kEmptyChild) push(c3);
+            if (c2 != kEmptyChild) push(c2);
+            if (c1 != kEmptyChild) push(c1);
+            if (c0 != kEmptyChild) {
+                cur = c0;
+                continue;
             }
-            h0 = false;
-        }
-        if (h1 && c1 < 0) {
-            int ti = ~c1;
-            float t, u, v;
-            bool bk;
-            float4 A = S.tri[3 * ti], B = S.tri[3 * ti + 1], C = S.tri[3 * ti + 2];
-            if (tri_intersect(A, B, C, o, d, tmin, best, t, u, v, bk)) {
-                int oi = __float_as_int(A.w);
-                if (ANY) { h.tri = ti; h.orig = oi; return true; }
-                if (t < best || oi < h.orig) {
-                    best = t; h.t = t; h.u = u; h.v = v; h.back = bk; h.tri = ti; h.orig = oi;
-                }
-            }
-            h1 = false;
-        }
-        if (h0 && h1) {
-            int nearc = (t0 <= t1) ? c0 : c1;
-            int farc = (t0 <= t1) ? c1 : c0;
-            if (sp < kStack) stack[sp++] = farc;
-            node = nearc;
-        } else if (h0) {
-            node = c0;
-        } else if (h1) {
-            node = c1;
         } else {
-            if (sp == 0) break;
-            node = stack[--sp];
+            const int first = leaf_first(cur), cnt = leaf_count(cur);
+            for (int k = 0; k < cnt; ++k) {
+                const int ti = first + k;
+                if (STATS) ts.tris++;
+                const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+                float t, u, v;
+                bool bk;
+                if (tri_intersect(A, E1, E2, o, d, tmin, best, t, u, v, bk)) {
+                    const int oi = __float_as_int(A.w);
+                    if (ANY) {
+                        h.tri = ti;
+                        h.orig = oi;
+                        return true;
+                    }
+                    if (t < best || oi < h.orig) {
+                        best = t; h.t = t; h.u = u; h.v = v; h.back = bk; h.tri = ti; h.orig = oi;
+                    }
+                }
+            }
         }
+        if (sp == 0) break;
+        --sp;
+        cur = sp < kStackDepth ? stk[sp * stride] : spill[sp - kStackDepth];
     }
     return h.tri >= 0;
 }
@@ -210,16 +237,17 @@ struct SurfaceHit {
 
 __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 d, SurfaceHit& s) {
     const int ti = h.tri;
-    const float4 A = S.tri[3 * ti], B = S.tri[3 * ti + 1], C = S.tri[3 * ti + 2];
-    const float4 NA = S.nrm[3 * ti], NB = S.nrm[3 * ti + 1], NC = S.nrm[3 * ti + 2];
-    const int mi = __float_as_int(B.w);
+    const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+    const float4 S0 = S.shade[4 * ti], S1 = S.shade[4 * ti + 1], S2 = S.shade[4 * ti + 2], S3 = S.shade[4 * ti + 3];
+    const int mi = __float_as_int(E1.w);
     const float4 M0 = S.mats[2 * mi], M1 = S.mats[2 * mi + 1];
     f3 wo_w = normalize(-d);
-    f3 v0 = mk(A.x, A.y, A.z), v1 = mk(B.x, B.y, B.z), v2 = mk(C.x, C.y, C.z);
-    f3 Ng = cross(v1 - v0, v2 - v0);
+    f3 v0 = mk(A.x, A.y, A.z), v1 = mk(S0.x, S0.y, S0.z), v2 = mk(S1.x, S1.y, S1.z);
+    f3 n0 = mk(S0.w, S1.w, S2.x), n1 = mk(S2.y, S2.z, S2.w), n2 = mk(S3.x, S3.y, S3.z);
+    f3 Ng = cross(mk(E1.x, E1.y, E1.z), mk(E2.x, E2.y, E2.z));
     const float u = h.u, v = h.v;
     float w = 1.0f - u - v;
-    f3 Ns = mk(w * NA.x + u * NB.x + v * NC.x, w * NA.y + u * NB.y + v * NC.y, w * NA.z + u * NB.z + v * NC.z);
+    f3 Ns = mk(w * n0.x + u * n1.x + v * n2.x, w * n0.y + u * n1.y + v * n2.y, w * n0.z + u * n1.z + v * n2.z);
     if (M1.y != 0.0f) Ns = normalize(Ns);  // has normals: normalize(modelMatrix * vec4(Ns, 0))
     if (dot(wo_w, Ng) < 0.0f) Ng = -Ng;
     Ng = normalize(Ng);
@@ -245,15 +273,15 @@ __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 
 }
 
 // One camera path: SamplePath (devicePrograms.cu:625-664) with the closest-hit program inlined.
-template <int MODE>
+template <int MODE, bool STATS>
 __device__ __forceinline__ f3 sample_path(const DevScene& S, const DevLaunch& L, f3 o, f3 d, uint32_t seed,
-                                          uint32_t& segs) {
+                                          uint32_t& segs, int* stk, int stride, TravStats& ts) {
     f3 radiance = mk(0, 0, 0), beta = mk(1, 1, 1);
     int bounce = 0;
     bool endPath = false;
     while (!endPath && bounce < L.max_bounces && length(beta) > 0.00001f) {
         Hit h;
-        bool hit = traverse<false>(S, o, d, 0.0f, 100.0f, h);
+        bool hit = traverse<false, STATS>(S, o, d, 0.0f, 100.0f, h, stk, stride, ts);
         segs++;
         if (!hit) {  // __miss__radiance :576-583
             beta = mk(0, 0, 0);
@@ -286,7 +314,7 @@ __device__ __forceinline__ f3 sample_path(const DevScene& S, const DevLaunch& L,
             f3 ldn = normalize(ldir);
             f3 so = sf.pos + 1e-3f * sf.ng;
             Hit sh;
-            bool occluded = traverse<true>(S, so, normalize(ldir), 0.0f, length(ldir), sh);
+            bool occluded = traverse<true, STATS>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
             f3 lds = to_local(sf.fr, ldn);
             if (!occluded) {
                 f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);

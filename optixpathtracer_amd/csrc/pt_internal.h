@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pt_device.h"
 
 namespace pt {
@@ -15,11 +17,13 @@ struct BuildInput {
     float cmin[3], cmax[3];  // centroid bounds (Morton quantisation range)
 };
 
-// LBVH in leaf order.
+// BVH4 (collapsed LBVH) + triangle records in leaf order.
 struct BuildOutput {
-    BNode* nodes;  // n-1
-    float4* tri;   // 3n
-    float4* nrm;   // 3n
+    BNode4* nodes;  // capacity max(1, n) nodes
+    float4* isect;  // 3n
+    float4* shade;  // 4n
+    int n_nodes;    // written by lbvh_build
+    int depth;      // BVH4 levels
 };
 
 // GPU LBVH build (Morton codes -> radix sort -> Karras 2012 hierarchy -> AABBs from a sparse
@@ -27,8 +31,32 @@ struct BuildOutput {
 // Returns hipSuccess or the first error; *ms = device time of the build.
 hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream, float* ms);
 
+// Wavefront path state: SoA queues in HBM, capacity = paths (one path per pixel per frame).
+struct WFState {
+    float4* ray_o[2] = {nullptr, nullptr};  // queue b&1: origin.xyz | path id
+    float4* ray_d[2] = {nullptr, nullptr};  // direction.xyz | 0
+    float4* hit = nullptr;                  // t, u, v, tri | back<<31 (or -1 = miss), queue order
+    float4* beta = nullptr;                 // path throughput.xyz | seed, path order
+    float4* L = nullptr;                    // path radiance of the frame, path order
+    float4* sh_o = nullptr;                 // shadow queue: origin | path
+    float4* sh_d = nullptr;                 // direction | tmax
+    float4* sh_c = nullptr;                 // deferred NEE contribution (fused modes)
+    int* aux = nullptr;                     // light index << 1 | conductor (RNG-coupled modes)
+    int* vis = nullptr;                     // shadow result per path (RNG-coupled modes)
+    int* count = nullptr;                   // [2b] queue length of bounce b, [2b+1] shadow count
+    int paths = 0;
+    int max_bounces = 0;
+};
+size_t wavefront_bytes(int paths, int max_bounces);
+hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces);
+void wavefront_free(WFState& W);
+// Enqueue one frame (all bounces) of the wavefront pipeline; adds the frame into L.accum.
+hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
+                                  uint32_t frame, int cus, hipStream_t stream);
+
 // Render launches.
-hipError_t launch_render(int kernel, int mode, const DevScene& S, const DevLaunch& L, hipStream_t stream);
+hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,
+                         hipStream_t stream);
 hipError_t launch_trace(const DevScene& S, const float* d_rays, int n, int* d_prim, float* d_thit, float* d_u,
                         float* d_v, int* d_back, int any_hit, hipStream_t stream);
 

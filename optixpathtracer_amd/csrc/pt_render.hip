@@ -6,12 +6,15 @@
 // tile, each wave64 an 8x8 quadrant (primary-ray coherence inside the wave).  The thread
 // loads its fp32 sum, adds the radiance of frame ids frame_base .. frame_base+n_frames-1
 // in order (identical rounding to sequential per-frame accumulation), and stores it once:
-// no per-spp HBM round trip of the 24.9 MB colour buffer.
+// no per-spp HBM round trip of the 24.9 MB colour buffer.  The BVH4 traversal stack lives
+// in LDS (32 entries x 256 threads = 32 KB per workgroup).
 #include "pt_internal.h"
 
 namespace pt {
 
 namespace {
+
+constexpr int kBlock = 256;
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
@@ -19,13 +22,34 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void k_render_mega(DevScene S, DevLaunch L) {
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(const DevLaunch& L, uint32_t segs, const TravStats& ts, int lane) {
+    unsigned long long a = wave_sum((unsigned long long)segs);
+    if (STATS) {
+        unsigned long long b = wave_sum((unsigned long long)ts.nodes);
+        unsigned long long c = wave_sum((unsigned long long)ts.tris);
+        unsigned long long d = wave_sum((unsigned long long)ts.rays);
+        unsigned long long e = wave_sum((unsigned long long)ts.overflow);
+        if (lane == 0 && L.counters) {
+            atomicAdd(&L.counters[1], b);
+            atomicAdd(&L.counters[2], c);
+            atomicAdd(&L.counters[3], d);
+            atomicAdd(&L.counters[4], e);
+        }
+    }
+    if (lane == 0 && L.counters) atomicAdd(&L.counters[0], a);
+}
+
+template <int MODE, bool STATS>
+__global__ __launch_bounds__(kBlock) void k_render_mega(DevScene S, DevLaunch L) {
+    __shared__ int stack[kStackDepth * kBlock];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    int* stk = stack + threadIdx.x;
     uint32_t segs = 0;
+    TravStats ts;
     if (x < L.width && y < L.height) {
         f3 o, d;
         camera_ray(L, x, y, o, d);
@@ -34,7 +58,7 @@ __global__ __launch_bounds__(256) void k_render_mega(DevScene S, DevLaunch L) {
         const uint32_t pix = (uint32_t)(L.width * y + x);
         for (uint32_t f = 0; f < L.n_frames; ++f) {
             uint32_t seed = tea16(pix, L.frame_base + f);  // devicePrograms.cu:631
-            f3 r = sample_path<MODE>(S, L, o, d, seed, segs);
+            f3 r = sample_path<MODE, STATS>(S, L, o, d, seed, segs, stk, kBlock, ts);
             sx += r.x;
             sy += r.y;
             sz += r.z;
@@ -43,18 +67,21 @@ __global__ __launch_bounds__(256) void k_render_mega(DevScene S, DevLaunch L) {
         L.accum[idx + 1] = sy;
         L.accum[idx + 2] = sz;
     }
-    unsigned long long tot = wave_sum((unsigned long long)segs);
-    if (lane == 0 && L.counters) atomicAdd(&L.counters[0], tot);
+    flush_stats<STATS>(L, segs, ts, lane);
 }
 
-__global__ __launch_bounds__(256) void k_trace(DevScene S, const float* rays, int n, int* prim, float* th,
-                                               float* uh, float* vh, int* back, int any_hit) {
+__global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays, int n, int* prim, float* th,
+                                                  float* uh, float* vh, int* back, int any_hit) {
+    __shared__ int stack[kStackDepth * kBlock];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* r = rays + 8 * (size_t)i;
     f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
     Hit h;
-    bool hit = any_hit ? traverse<true>(S, o, d, r[6], r[7], h) : traverse<false>(S, o, d, r[6], r[7], h);
+    TravStats ts;
+    int* stk = stack + threadIdx.x;
+    bool hit = any_hit ? traverse<true, false>(S, o, d, r[6], r[7], h, stk, kBlock, ts)
+                       : traverse<false, false>(S, o, d, r[6], r[7], h, stk, kBlock, ts);
     prim[i] = hit ? h.orig : -1;
     th[i] = hit && !any_hit ? h.t : 0.0f;
     uh[i] = hit && !any_hit ? h.u : 0.0f;
@@ -63,30 +90,34 @@ __global__ __launch_bounds__(256) void k_trace(DevScene S, const float* rays, in
 }
 
 template <int MODE>
-hipError_t launch_mega(const DevScene& S, const DevLaunch& L, hipStream_t stream) {
+hipError_t launch_mega(const DevScene& S, const DevLaunch& L, bool stats, hipStream_t stream) {
     dim3 grid((unsigned)((L.width + 15) / 16), (unsigned)((L.height + 15) / 16));
-    hipLaunchKernelGGL(k_render_mega<MODE>, grid, dim3(256), 0, stream, S, L);
+    if (stats)
+        hipLaunchKernelGGL((k_render_mega<MODE, true>), grid, dim3(kBlock), 0, stream, S, L);
+    else
+        hipLaunchKernelGGL((k_render_mega<MODE, false>), grid, dim3(kBlock), 0, stream, S, L);
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_render(int kernel, int mode, const DevScene& S, const DevLaunch& L, hipStream_t stream) {
+hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,
+                         hipStream_t stream) {
     (void)kernel;
     switch (mode) {
-        case kModeLambert: return launch_mega<kModeLambert>(S, L, stream);
-        case kModeConductor: return launch_mega<kModeConductor>(S, L, stream);
-        case kModeDielectric: return launch_mega<kModeDielectric>(S, L, stream);
-        case kModeLayered: return launch_mega<kModeLayered>(S, L, stream);
-        default: return launch_mega<kModeDefault>(S, L, stream);
+        case kModeLambert: return launch_mega<kModeLambert>(S, L, stats, stream);
+        case kModeConductor: return launch_mega<kModeConductor>(S, L, stats, stream);
+        case kModeDielectric: return launch_mega<kModeDielectric>(S, L, stats, stream);
+        case kModeLayered: return launch_mega<kModeLayered>(S, L, stats, stream);
+        default: return launch_mega<kModeDefault>(S, L, stats, stream);
     }
 }
 
 hipError_t launch_trace(const DevScene& S, const float* d_rays, int n, int* d_prim, float* d_thit, float* d_u,
                         float* d_v, int* d_back, int any_hit, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, S, d_rays, n, d_prim,
-                       d_thit, d_u, d_v, d_back, any_hit);
+    hipLaunchKernelGGL(k_trace, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, S, d_rays, n,
+                       d_prim, d_thit, d_u, d_v, d_back, any_hit);
     return hipGetLastError();
 }
 

@@ -1,0 +1,475 @@
+// pt_wavefront.hip — wavefront path tracer for gfx950 (PT_KERNEL_WAVEFRONT).
+//
+// The reference runs one OptiX thread per pixel that loops over bounces
+// (SamplePath, devicePrograms.cu:625-664).  Here each bounce of a frame is a sequence of
+// persistent, grid-stride kernels over SoA queues in HBM, so the traversal kernels carry
+// only a ray (low VGPR count -> high occupancy) and the BSDF code runs in its own kernel:
+//
+//   k_camera            : path p = pixel p of the frame; camera ray -> queue 0, state init
+//   per bounce b:
+//     k_extend          : closest hit of queue b (BVH4 traversal, LDS stack) -> hit records
+//     fused modes (Lambert / Conductor / Dielectric: BRDF eval draws no random numbers):
+//       k_shade_fused   : surface, metallic coin, light pick, f*|cos|, BSDF sample; NEE
+//                         contribution + shadow ray -> shadow queue (only if f != 0);
+//                         continuation ray -> queue b+1 (wave-ballot compaction)
+//       k_shadow_add    : any-hit; unoccluded -> L[path] += contribution
+//     RNG-coupled modes (Default / Layered: GlossyDiffuse::f consumes the path seed only
+//     when the light is visible, GlossyDiffuse.h:230-343):
+//       k_shade_a       : surface, coin, light pick -> shadow ray queue
+//       k_shadow_vis    : any-hit -> vis[path]
+//       k_shade_b       : if visible: f (may draw), NEE; BSDF sample -> queue b+1
+//   k_accum             : accum[pixel] += L[path]   (one frame at a time: same fp32 order as
+//                         the sequential reference accumulation)
+//
+// Every kernel reads queue lengths from device memory written by an earlier launch (kernel
+// boundaries order the hand-off), so a whole frame is enqueued without host round trips.
+#include "pt_internal.h"
+
+namespace pt {
+
+namespace {
+
+constexpr int kBlockWF = 256;
+constexpr int kMissTri = -1;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Wave-wide compaction: every active lane of the wave calls this (converged); lanes with
+// pred get consecutive slots.  One atomic per wave.
+__device__ __forceinline__ int wave_append(int* counter, bool pred) {
+    const unsigned long long m = __ballot(pred ? 1 : 0);
+    const int cnt = __popcll(m);
+    int base = 0;
+    if (cnt > 0) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        if (lane_id() == leader) base = atomicAdd(counter, cnt);
+        base = __shfl(base, leader, 64);
+    }
+    const int prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    return base + prefix;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Per-bounce counter block (kCnt ints): queue length, shadow-queue length, and one
+// work-fetch head per kernel of the bounce (zeroed by the per-frame memset).
+constexpr int kCnt = 8;
+enum { kQueue = 0, kShadowQ = 1, kFetchExtend = 2, kFetchShade = 3, kFetchShadow = 4, kFetchShadeB = 5 };
+__device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + kCnt * b + k; }
+
+// Work distribution: one queue item per thread over a grid sized to the queue capacity;
+// waves past the live queue length exit at once and the hardware dispatcher balances the
+// divergent rest.  (Measured alternatives, see DESIGN.md: persistent grids with one atomic
+// fetch head per kernel serialise on the head — MI355X_MICROARCH.md "dequeue" — and
+// chunked fetching starves waves.)
+#define WF_LOOP(i, valid, n, head)                                                                   \
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x), valid = (i < (n)), i##_once = 1;       \
+         i##_once && __any(valid); i##_once = 0)
+
+__global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame) {
+    const int P = L.width * L.height;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        const int x = p % L.width, y = p / L.width;
+        f3 o, d;
+        camera_ray(L, x, y, o, d);
+        W.ray_o[0][p] = make_float4(o.x, o.y, o.z, __int_as_float(p));
+        W.ray_d[0][p] = make_float4(d.x, d.y, d.z, 0.0f);
+        const uint32_t seed = tea16((uint32_t)(L.width * y + x), frame);  // devicePrograms.cu:631
+        W.beta[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(seed));
+        W.L[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kQueue) = P;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(kBlockWF) void k_extend(DevScene S, WFState W, int b, unsigned long long* counters) {
+    __shared__ int stack[kStackDepth * kBlockWF];
+    const int n = *cnt(W, b, kQueue);
+    const float4* ro = W.ray_o[b & 1];
+    const float4* rd = W.ray_d[b & 1];
+    int* stk = stack + threadIdx.x;
+    TravStats ts;
+    WF_LOOP(i, valid, n, cnt(W, b, kFetchExtend)) {
+        if (valid) {
+            const float4 a = ro[i], c = rd[i];
+            Hit h;
+            bool hit = traverse<false, STATS>(S, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f, h, stk,
+                                              kBlockWF, ts);
+            W.hit[i] = hit ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                           : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[0], (unsigned long long)n);
+    if (STATS && counters) {
+        unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
+        unsigned long long e = wave_sum_u64(ts.overflow);
+        if (lane_id() == 0) {
+            atomicAdd(&counters[1], a);
+            atomicAdd(&counters[2], c);
+            atomicAdd(&counters[3], d);
+            atomicAdd(&counters[4], e);
+        }
+    }
+}
+
+__device__ __forceinline__ Hit decode_hit(float4 hv) {
+    Hit h;
+    const int code = __float_as_int(hv.w);
+    h.t = hv.x;
+    h.u = hv.y;
+    h.v = hv.z;
+    h.back = code != kMissTri && (code & (int)0x80000000);
+    h.tri = code == kMissTri ? -1 : (code & 0x7fffffff);
+    return h;
+}
+
+// light choice: Lighting::GetRandomPointLight (LightMethods.h:25-40)
+__device__ __forceinline__ float pick_light(const DevLaunch& L, uint32_t& seed, int& li) {
+    li = 0;
+    if (L.n_lights == 1) return 1.0f;
+    if (L.n_lights <= 0) return 0.0f;
+    float r = rnd(seed);
+    li = (int)(r * (float)L.n_lights);
+    if (li >= L.n_lights) li = L.n_lights - 1;
+    return 1.0f / (float)L.n_lights;
+}
+
+// continuation (devicePrograms.cu:501-509) + loop test of SamplePath (:646)
+__device__ __forceinline__ bool continue_path(const SurfaceHit& sf, const BSample& bs, f3& beta, f3& o, f3& d,
+                                              int next_bounce, int max_bounces) {
+    float ac = abs_dot(bs.dir, mk(0.0f, 0.0f, 1.0f));
+    beta = beta * mk(bs.color.x * ac / bs.pdf, bs.color.y * ac / bs.pdf, bs.color.z * ac / bs.pdf);
+    f3 off = 1e-3f * sf.ng;
+    if (dot(bs.dir, mk(0.0f, 0.0f, 1.0f)) < 0.0f) off = -off;
+    o = sf.pos + off;
+    d = normalize(to_world(sf.fr, bs.dir));
+    return next_bounce < max_bounces && length(beta) > 0.00001f;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlockWF) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b) {
+    const int n = *cnt(W, b, kQueue);
+    const float4* ro = W.ray_o[b & 1];
+    const float4* rd = W.ray_d[b & 1];
+    float4* no = W.ray_o[(b + 1) & 1];
+    float4* nd = W.ray_d[(b + 1) & 1];
+    WF_LOOP(i, valid, n, cnt(W, b, kFetchShade)) {
+        bool emit_shadow = false, emit_next = false;
+        f3 so, sdir, contrib, o, d;
+        float stmax = 0.0f;
+        int path = 0;
+        if (valid) {
+            const float4 a = ro[i], c = rd[i];
+            path = __float_as_int(a.w);
+            const Hit h = decode_hit(W.hit[i]);
+            if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
+                d = mk(c.x, c.y, c.z);
+                SurfaceHit sf;
+                reconstruct(S, h, d, sf);
+                float4 bv = W.beta[path];
+                uint32_t seed = __float_as_uint(bv.w);
+                f3 beta = mk(bv.x, bv.y, bv.z);
+                const bool conductor = rnd(seed) < sf.metallic;  // :400
+                int li;
+                const float P = pick_light(L, seed, li);
+                if (P > 0.0f) {
+                    const DevLight lt = L.lights[li];
+                    f3 lpos = mk(lt.px, lt.py, lt.pz);
+                    f3 ldir = lpos - sf.pos;
+                    f3 ldn = normalize(ldir);
+                    f3 lds = to_local(sf.fr, ldn);
+                    // f has no RNG side effects in these modes: evaluate before the shadow test
+                    f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);
+                    f3 spectrum = f * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+                    if (!is_zero(spectrum)) {
+                        f3 dd = sf.pos - lpos;
+                        float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+                        f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+                        contrib = ((beta * spectrum) * Li) / (P * 1.0f);
+                        so = sf.pos + 1e-3f * sf.ng;
+                        sdir = normalize(ldir);
+                        stmax = length(ldir);
+                        emit_shadow = true;
+                    }
+                }
+                BSample bs;
+                if (bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
+                    emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
+                    W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
+                }
+            }
+        }
+        const int si = wave_append(cnt(W, b, kShadowQ), emit_shadow);
+        if (emit_shadow) {
+            W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(path));
+            W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
+            W.sh_c[si] = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+        }
+        const int qi = wave_append(cnt(W, b + 1, kQueue), emit_next);
+        if (emit_next) {
+            no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
+            nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlockWF) void k_shadow_add(DevScene S, WFState W, int b) {
+    __shared__ int stack[kStackDepth * kBlockWF];
+    const int n = *cnt(W, b, kShadowQ);
+    int* stk = stack + threadIdx.x;
+    TravStats ts;
+    WF_LOOP(j, valid, n, cnt(W, b, kFetchShadow)) {
+        if (valid) {
+            const float4 a = W.sh_o[j], c = W.sh_d[j];
+            Hit h;
+            bool occluded = traverse<true, false>(S, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w, h, stk,
+                                                  kBlockWF, ts);
+            if (!occluded) {
+                const int path = __float_as_int(a.w);
+                const float4 k = W.sh_c[j];
+                float4 l = W.L[path];
+                W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
+            }
+        }
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlockWF) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b) {
+    const int n = *cnt(W, b, kQueue);
+    const float4* ro = W.ray_o[b & 1];
+    const float4* rd = W.ray_d[b & 1];
+    WF_LOOP(i, valid, n, cnt(W, b, kFetchShade)) {
+        bool emit = false;
+        f3 so, sdir;
+        float stmax = 0.0f;
+        int path = 0;
+        if (valid) {
+            const float4 a = ro[i], c = rd[i];
+            path = __float_as_int(a.w);
+            const Hit h = decode_hit(W.hit[i]);
+            if (h.tri >= 0) {
+                SurfaceHit sf;
+                reconstruct(S, h, mk(c.x, c.y, c.z), sf);
+                float4 bv = W.beta[path];
+                uint32_t seed = __float_as_uint(bv.w);
+                const bool conductor = rnd(seed) < sf.metallic;
+                int li;
+                const float P = pick_light(L, seed, li);
+                W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));
+                W.aux[path] = (li << 1) | (conductor ? 1 : 0);
+                if (P > 0.0f) {
+                    const DevLight lt = L.lights[li];
+                    f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
+                    so = sf.pos + 1e-3f * sf.ng;
+                    sdir = normalize(ldir);
+                    stmax = length(ldir);
+                    emit = true;
+                }
+            }
+        }
+        const int si = wave_append(cnt(W, b, kShadowQ), emit);
+        if (emit) {
+            W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(path));
+            W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlockWF) void k_shadow_vis(DevScene S, WFState W, int b) {
+    __shared__ int stack[kStackDepth * kBlockWF];
+    const int n = *cnt(W, b, kShadowQ);
+    int* stk = stack + threadIdx.x;
+    TravStats ts;
+    WF_LOOP(j, valid, n, cnt(W, b, kFetchShadow)) {
+        if (valid) {
+            const float4 a = W.sh_o[j], c = W.sh_d[j];
+            Hit h;
+            bool occluded = traverse<true, false>(S, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w, h, stk,
+                                                  kBlockWF, ts);
+            W.vis[__float_as_int(a.w)] = occluded ? 0 : 1;
+        }
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlockWF) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
+    const int n = *cnt(W, b, kQueue);
+    const float4* ro = W.ray_o[b & 1];
+    const float4* rd = W.ray_d[b & 1];
+    float4* no = W.ray_o[(b + 1) & 1];
+    float4* nd = W.ray_d[(b + 1) & 1];
+    WF_LOOP(i, valid, n, cnt(W, b, kFetchShadeB)) {
+        bool emit_next = false;
+        f3 o, d;
+        int path = 0;
+        if (valid) {
+            const float4 a = ro[i], c = rd[i];
+            path = __float_as_int(a.w);
+            const Hit h = decode_hit(W.hit[i]);
+            if (h.tri >= 0) {
+                d = mk(c.x, c.y, c.z);
+                SurfaceHit sf;
+                reconstruct(S, h, d, sf);
+                float4 bv = W.beta[path];
+                uint32_t seed = __float_as_uint(bv.w);
+                f3 beta = mk(bv.x, bv.y, bv.z);
+                const int aux = W.aux[path];
+                const bool conductor = aux & 1;
+                const int li = aux >> 1;
+                if (L.n_lights > 0 && W.vis[path]) {
+                    const float P = L.n_lights == 1 ? 1.0f : 1.0f / (float)L.n_lights;
+                    const DevLight lt = L.lights[li];
+                    f3 lpos = mk(lt.px, lt.py, lt.pz);
+                    f3 lds = to_local(sf.fr, normalize(lpos - sf.pos));
+                    f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);
+                    f3 spectrum = f * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+                    if (!is_zero(spectrum)) {
+                        f3 dd = sf.pos - lpos;
+                        float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+                        f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+                        f3 add = ((beta * spectrum) * Li) / (P * 1.0f);
+                        float4 l = W.L[path];
+                        W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
+                    }
+                }
+                BSample bs;
+                if (bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
+                    emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
+                    W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
+                }
+            }
+        }
+        const int qi = wave_append(cnt(W, b + 1, kQueue), emit_next);
+        if (emit_next) {
+            no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
+            nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L) {
+    const int P = L.width * L.height;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        const float4 l = W.L[p];
+        const size_t idx = (size_t)p * 3;
+        L.accum[idx] += l.x;
+        L.accum[idx + 1] += l.y;
+        L.accum[idx + 2] += l.z;
+    }
+}
+
+inline bool fused_mode(int mode) { return mode == kModeLambert || mode == kModeConductor || mode == kModeDielectric; }
+
+// Grid covering `items` queue slots (one per thread).
+template <typename K>
+dim3 resident_grid(K, int cus, int items) {
+    (void)cus;
+    return dim3((unsigned)std::max(1, (items + kBlockWF - 1) / kBlockWF));
+}
+
+template <int MODE>
+hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int cus,
+                        int items, hipStream_t stream, int phase) {
+    if (fused) {
+        if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
+            hipLaunchKernelGGL((k_shade_fused<MODE>), resident_grid(k_shade_fused<MODE>, cus, items), dim3(kBlockWF),
+                               0, stream, S, L, W, b);
+    } else if (phase == 0) {
+        hipLaunchKernelGGL((k_shade_a<MODE>), resident_grid(k_shade_a<MODE>, cus, items), dim3(kBlockWF), 0, stream,
+                           S, L, W, b);
+    } else {
+        hipLaunchKernelGGL((k_shade_b<MODE>), resident_grid(k_shade_b<MODE>, cus, items), dim3(kBlockWF), 0, stream,
+                           S, L, W, b);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b,
+                             int cus, int items, hipStream_t stream, int phase) {
+    switch (mode) {
+        case kModeLambert: return launch_shade<kModeLambert>(fused, S, L, W, b, cus, items, stream, phase);
+        case kModeConductor: return launch_shade<kModeConductor>(fused, S, L, W, b, cus, items, stream, phase);
+        case kModeDielectric: return launch_shade<kModeDielectric>(fused, S, L, W, b, cus, items, stream, phase);
+        case kModeLayered: return launch_shade<kModeLayered>(fused, S, L, W, b, cus, items, stream, phase);
+        default: return launch_shade<kModeDefault>(fused, S, L, W, b, cus, items, stream, phase);
+    }
+}
+
+}  // namespace
+
+size_t wavefront_bytes(int paths, int max_bounces) {
+    size_t P = (size_t)paths;
+    return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 2 /*beta, L*/ + 3 /*shadow*/) +
+           P * 2 * sizeof(int) + sizeof(int) * kCnt * (size_t)(max_bounces + 2);
+}
+
+hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
+    size_t P = (size_t)paths;
+    hipError_t e = hipSuccess;
+    auto al = [&](void** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc(p, bytes > 0 ? bytes : 16);
+    };
+    al((void**)&W.ray_o[0], P * sizeof(float4));
+    al((void**)&W.ray_o[1], P * sizeof(float4));
+    al((void**)&W.ray_d[0], P * sizeof(float4));
+    al((void**)&W.ray_d[1], P * sizeof(float4));
+    al((void**)&W.hit, P * sizeof(float4));
+    al((void**)&W.beta, P * sizeof(float4));
+    al((void**)&W.L, P * sizeof(float4));
+    al((void**)&W.sh_o, P * sizeof(float4));
+    al((void**)&W.sh_d, P * sizeof(float4));
+    al((void**)&W.sh_c, P * sizeof(float4));
+    al((void**)&W.aux, P * sizeof(int));
+    al((void**)&W.vis, P * sizeof(int));
+    al((void**)&W.count, sizeof(int) * kCnt * (size_t)(max_bounces + 2));
+    W.paths = paths;
+    W.max_bounces = max_bounces;
+    return e;
+}
+
+void wavefront_free(WFState& W) {
+    void* ps[] = {W.ray_o[0], W.ray_o[1], W.ray_d[0], W.ray_d[1], W.hit, W.beta, W.L, W.sh_o, W.sh_d, W.sh_c,
+                  W.aux, W.vis, W.count};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    W = WFState{};
+}
+
+hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
+                                  uint32_t frame, int cus, hipStream_t stream) {
+    const int P = L.width * L.height;
+    const int maxb = L.max_bounces;
+    hipError_t e = hipMemsetAsync(W.count, 0, sizeof(int) * kCnt * (size_t)(maxb + 2), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_camera, resident_grid(k_camera, cus, P), dim3(kBlockWF), 0, stream, W, L, frame);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const bool fused = fused_mode(mode);
+    for (int b = 0; b < maxb; ++b) {
+        if (stats)
+            hipLaunchKernelGGL(k_extend<true>, resident_grid(k_extend<true>, cus, P), dim3(kBlockWF), 0, stream, S, W,
+                               b, L.counters);
+        else
+            hipLaunchKernelGGL(k_extend<false>, resident_grid(k_extend<false>, cus, P), dim3(kBlockWF), 0, stream, S,
+                               W, b, L.counters);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (fused) {
+            if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_shadow_add, resident_grid(k_shadow_add, cus, P), dim3(kBlockWF), 0, stream, S, W, b);
+        } else {
+            if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_shadow_vis, resident_grid(k_shadow_vis, cus, P), dim3(kBlockWF), 0, stream, S, W, b);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 1)) != hipSuccess) return e;
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_accum, resident_grid(k_accum, cus, P), dim3(kBlockWF), 0, stream, W, L);
+    return hipGetLastError();
+}
+
+}  // namespace pt

@@ -74,7 +74,7 @@ class OptixRenderer:
     """Drop-in for `OptixRenderer` (OptixRenderer.h:8-110) backed by libptamd.so."""
 
     def __init__(self, ptx_path_or_none, model: Scene, device: int = 0, material_mode: int | None = None,
-                 kernel: int = capi.PT_KERNEL_MEGA):
+                 kernel: int = capi.PT_KERNEL_AUTO):
         # ptxPath is accepted for signature compatibility and ignored (no PTX on gfx950).
         self.lib = load()
         self.model = model
@@ -133,6 +133,9 @@ class OptixRenderer:
 
     def set_frames_per_launch(self, frames: int) -> None:
         check(self.lib.pt_set_frames_per_launch(self.h, int(frames)), "pt_set_frames_per_launch")
+
+    def set_traversal_stats(self, enable: bool) -> None:
+        check(self.lib.pt_set_traversal_stats(self.h, 1 if enable else 0), "pt_set_traversal_stats")
 
     def accum_clear(self) -> None:
         check(self.lib.pt_accum_clear(self.h), "pt_accum_clear")
@@ -197,7 +200,7 @@ class OptixRenderer:
 
 
 def setup_renderer(scene: Scene, width: int, height: int, max_bounces: int, device: int = 0,
-                   kernel: int = capi.PT_KERNEL_MEGA) -> OptixRenderer:
+                   kernel: int = capi.PT_KERNEL_AUTO) -> OptixRenderer:
     """The reference's main.cpp:95-113 sequence: construct, Resize, SetLights, SetMaxBounces, SetCamera."""
     r = OptixRenderer(None, scene, device=device, kernel=kernel)
     r.Resize((width, height))

@@ -167,3 +167,27 @@ def test_determinism_fullhd_properties(diffuse_scene):
     o, _ = oracle_render(diffuse_scene, 1920, 1080, 8, 1, 2, rect=(0, 532, 1920, 548))
     band = slice(532, 548)
     assert image_mse(g1[band] / 2, o[band] / 2) <= MSE_TOL
+
+
+@pytest.mark.parametrize("variant", ["diffuse", "conductor", "dielectric20", "layered"])
+def test_wavefront_bit_identical_to_megakernel(variant):
+    """Both kernel designs add each path's NEE terms in bounce order and accumulate frames
+    in order, so their images must agree bit for bit (and hence with the oracle parity)."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene(variant)
+    a, sa = gpu_render(sc, 64, 48, 5, 3, 6, kernel=0)
+    b, sb = gpu_render(sc, 64, 48, 5, 3, 6, kernel=1)
+    np.testing.assert_array_equal(a, b)
+    assert sa["segments"] == sb["segments"]
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_wavefront_config1_parity(diffuse_scene, mode):
+    g, st = gpu_render(diffuse_scene, 256, 256, 4, 1, 16, mode=mode, kernel=1)
+    o, segs = oracle_render(diffuse_scene, 256, 256, 4, 1, 16, mode=mode)
+    mse = image_mse(g / 16, o / 16)
+    assert mse <= MSE_TOL, mse
+    assert close_fraction(g, o) >= CLOSE_MIN
+    m, _ = gpu_render(diffuse_scene, 256, 256, 4, 1, 16, mode=mode, kernel=0)
+    np.testing.assert_array_equal(g, m)
