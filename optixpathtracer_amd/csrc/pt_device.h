@@ -272,75 +272,92 @@ __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 
     s.roughness = M1.x;
 }
 
-// One camera path: SamplePath (devicePrograms.cu:625-664) with the closest-hit program inlined.
+// Path state of one camera sample (RadianceRayData, RayData.h:5-21).
+struct PathState {
+    f3 o, d, beta, radiance;
+    uint32_t seed;
+    int bounce;
+    bool end;
+};
+
+__device__ __forceinline__ void path_start(PathState& p, f3 o, f3 d, uint32_t seed) {  // SamplePath :626-635
+    p.o = o;
+    p.d = d;
+    p.beta = mk(1.0f, 1.0f, 1.0f);
+    p.radiance = mk(0.0f, 0.0f, 0.0f);
+    p.seed = seed;
+    p.bounce = 0;
+    p.end = false;
+}
+
+// loop test of SamplePath (devicePrograms.cu:646)
+__device__ __forceinline__ bool path_alive(const DevLaunch& L, const PathState& p) {
+    return !p.end && p.bounce < L.max_bounces && length(p.beta) > 0.00001f;
+}
+
+// One iteration of SamplePath's loop: TraceRadiance + __closesthit__radiance
+// (devicePrograms.cu:343-514) or __miss__radiance (:576-583).  Returns false on a miss.
 template <int MODE, bool STATS>
-__device__ __forceinline__ f3 sample_path(const DevScene& S, const DevLaunch& L, f3 o, f3 d, uint32_t seed,
-                                          uint32_t& segs, int* stk, int stride, TravStats& ts) {
-    f3 radiance = mk(0, 0, 0), beta = mk(1, 1, 1);
-    int bounce = 0;
-    bool endPath = false;
-    while (!endPath && bounce < L.max_bounces && length(beta) > 0.00001f) {
-        Hit h;
-        bool hit = traverse<false, STATS>(S, o, d, 0.0f, 100.0f, h, stk, stride, ts);
-        segs++;
-        if (!hit) {  // __miss__radiance :576-583
-            beta = mk(0, 0, 0);
-            bounce = 100;
-            continue;
-        }
-        bounce++;
-        if (bounce > L.max_bounces) {
-            endPath = true;
-            continue;
-        }
-        SurfaceHit sf;
-        reconstruct(S, h, d, sf);
-        const bool conductor = rnd(seed) < sf.metallic;  // :400
-        // NEE (:446-472), Lighting::GetRandomPointLight (LightMethods.h:25-40)
-        float P = 0.0f;
-        int li = 0;
-        if (L.n_lights == 1) {
-            P = 1.0f;
-        } else if (L.n_lights > 1) {
-            float r = rnd(seed);
-            li = (int)(r * (float)L.n_lights);
-            if (li >= L.n_lights) li = L.n_lights - 1;
-            P = 1.0f / (float)L.n_lights;
-        }
-        if (P > 0.0f) {
-            const DevLight lt = L.lights[li];
-            f3 lpos = mk(lt.px, lt.py, lt.pz);
-            f3 ldir = lpos - sf.pos;
-            f3 ldn = normalize(ldir);
-            f3 so = sf.pos + 1e-3f * sf.ng;
-            Hit sh;
-            bool occluded = traverse<true, STATS>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
-            f3 lds = to_local(sf.fr, ldn);
-            if (!occluded) {
-                f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);
-                float c = abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
-                f3 spectrum = f * c;
-                if (!is_zero(spectrum)) {
-                    f3 dd = sf.pos - lpos;
-                    float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
-                    f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
-                    radiance = radiance + ((beta * spectrum) * Li) / (P * 1.0f);
-                }
+__device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch& L, PathState& p, int* stk,
+                                             int stride, TravStats& ts) {
+    Hit h;
+    bool hit = traverse<false, STATS>(S, p.o, p.d, 0.0f, 100.0f, h, stk, stride, ts);
+    if (!hit) {
+        p.beta = mk(0, 0, 0);
+        p.bounce = 100;
+        return;
+    }
+    p.bounce++;
+    if (p.bounce > L.max_bounces) {
+        p.end = true;
+        return;
+    }
+    SurfaceHit sf;
+    reconstruct(S, h, p.d, sf);
+    const bool conductor = rnd(p.seed) < sf.metallic;  // :400
+    // NEE (:446-472), Lighting::GetRandomPointLight (LightMethods.h:25-40)
+    float P = 0.0f;
+    int li = 0;
+    if (L.n_lights == 1) {
+        P = 1.0f;
+    } else if (L.n_lights > 1) {
+        float r = rnd(p.seed);
+        li = (int)(r * (float)L.n_lights);
+        if (li >= L.n_lights) li = L.n_lights - 1;
+        P = 1.0f / (float)L.n_lights;
+    }
+    if (P > 0.0f) {
+        const DevLight lt = L.lights[li];
+        f3 lpos = mk(lt.px, lt.py, lt.pz);
+        f3 ldir = lpos - sf.pos;
+        f3 ldn = normalize(ldir);
+        f3 so = sf.pos + 1e-3f * sf.ng;
+        Hit sh;
+        bool occluded = traverse<true, STATS>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
+        f3 lds = to_local(sf.fr, ldn);
+        if (!occluded) {
+            f3 f = bsdf_f<MODE>(p.seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);
+            float c = abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+            f3 spectrum = f * c;
+            if (!is_zero(spectrum)) {
+                f3 dd = sf.pos - lpos;
+                float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+                f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+                p.radiance = p.radiance + ((p.beta * spectrum) * Li) / (P * 1.0f);
             }
         }
-        BSample bs;
-        if (!bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
-            endPath = true;
-            continue;
-        }
-        float ac = abs_dot(bs.dir, mk(0.0f, 0.0f, 1.0f));
-        beta = beta * mk(bs.color.x * ac / bs.pdf, bs.color.y * ac / bs.pdf, bs.color.z * ac / bs.pdf);
-        f3 off = 1e-3f * sf.ng;
-        if (dot(bs.dir, mk(0.0f, 0.0f, 1.0f)) < 0.0f) off = -off;
-        o = sf.pos + off;
-        d = normalize(to_world(sf.fr, bs.dir));
     }
-    return radiance;
+    BSample bs;
+    if (!bsdf_sample<MODE>(p.seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
+        p.end = true;
+        return;
+    }
+    float ac = abs_dot(bs.dir, mk(0.0f, 0.0f, 1.0f));
+    p.beta = p.beta * mk(bs.color.x * ac / bs.pdf, bs.color.y * ac / bs.pdf, bs.color.z * ac / bs.pdf);
+    f3 off = 1e-3f * sf.ng;
+    if (dot(bs.dir, mk(0.0f, 0.0f, 1.0f)) < 0.0f) off = -off;
+    p.o = sf.pos + off;
+    p.d = normalize(to_world(sf.fr, bs.dir));
 }
 
 }  // namespace pt

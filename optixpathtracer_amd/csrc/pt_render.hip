@@ -50,18 +50,29 @@ __global__ __launch_bounds__(kBlock) void k_render_mega(DevScene S, DevLaunch L)
     int* stk = stack + threadIdx.x;
     uint32_t segs = 0;
     TravStats ts;
-    if (x < L.width && y < L.height) {
-        f3 o, d;
-        camera_ray(L, x, y, o, d);
+    if (x < L.width && y < L.height && L.n_frames > 0) {
+        f3 co, cd;
+        camera_ray(L, x, y, co, cd);
         const size_t idx = ((size_t)y * (size_t)L.width + (size_t)x) * 3;
         float sx = L.accum[idx], sy = L.accum[idx + 1], sz = L.accum[idx + 2];
         const uint32_t pix = (uint32_t)(L.width * y + x);
-        for (uint32_t f = 0; f < L.n_frames; ++f) {
-            uint32_t seed = tea16(pix, L.frame_base + f);  // devicePrograms.cu:631
-            f3 r = sample_path<MODE, STATS>(S, L, o, d, seed, segs, stk, kBlock, ts);
-            sx += r.x;
-            sy += r.y;
-            sz += r.z;
+        // Path regeneration: a lane whose path ends starts its next frame at once instead of
+        // idling until the wave's longest path of the frame finishes.  Each lane still adds
+        // its frames in order, so the sum is bit-identical to the sequential accumulation.
+        uint32_t f = 0;
+        PathState p;
+        path_start(p, co, cd, tea16(pix, L.frame_base));  // devicePrograms.cu:631
+        while (true) {
+            if (path_alive(L, p)) {
+                path_segment<MODE, STATS>(S, L, p, stk, kBlock, ts);
+                segs++;
+                continue;
+            }
+            sx += p.radiance.x;
+            sy += p.radiance.y;
+            sz += p.radiance.z;
+            if (++f == L.n_frames) break;
+            path_start(p, co, cd, tea16(pix, L.frame_base + f));
         }
         L.accum[idx] = sx;
         L.accum[idx + 1] = sy;
