@@ -135,7 +135,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # PTAMD_LIB selects an alternative in-tree build (kernel A/B variants, tools/).
+    p = Path(path) if path else Path(os.environ.get("PTAMD_LIB", LIB_PATH))
     if not p.exists():
         raise PTError(
             f"{p} not found: the HIP extension is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)"

@@ -121,93 +121,195 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
     ta = t0; tb = t1; ca = c0; cb = c1;
 }
 
-// LDS stack: entry s of thread tid at stk[s * kStackStride] with stk = base + tid, so the
-// 64 lanes of a wave always touch 64 consecutive dwords (conflict-free for any sp mix).
-constexpr int kStackDepth = 32;
-constexpr int kSpillDepth = 64;
+// LDS stack: entry s of thread tid at stk[s * stride] with stk = base + tid, so the 64
+// lanes of a wave always touch 64 consecutive dwords (conflict-free for any sp mix).  Pushes
+// and pops only ever address LDS: when a push would overflow it, the bottom half moves to a
+// private spill array, and a pop from an empty LDS stack brings the newest spilled half
+// back (both rare, separate branches — a pop that may read either memory compiles to a
+// slow flat load on every step).
+// The LDS depth is a template parameter (DEPTH): it trades LDS per workgroup against
+// occupancy per kernel (see pt_render.hip / pt_wavefront.hip).
+constexpr int kSpillDepth = 64;  // spill + LDS hold a BVH4 path of depth > 20
+#ifndef PT_TRI_PREDICATED
+#define PT_TRI_PREDICATED 1
+#endif
 
-// Closest hit ordered by (t, original triangle index): independent of BVH shape.
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h,
-                                         int* __restrict__ stk, int stride, TravStats& ts) {
-    h.tri = -1;
-    h.orig = 0x7fffffff;
-    if (STATS) ts.rays++;
-    if (S.ntri <= 0) return false;
-    const f3 inv = safe_inv(d);
-    const f3 io = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-    float best = tmax;
-    int sp = 0;
-    int cur = 0;  // root (always an inner node)
-    // LDS holds the top kStackDepth entries; deeper ones (never seen on the benchmark
-    // scenes, see the overflow counter) go to a private spill array instead of being lost.
-    int spill[kSpillDepth];
-    auto push = [&](int c) {
-        if (sp < kStackDepth) stk[sp * stride] = c;
-        else if (sp < kStackDepth + kSpillDepth) spill[sp - kStackDepth] = c;
-        else { if (STATS) ts.overflow++; return; }
-        ++sp;
-    };
-    while (true) {
-        if (cur >= 0) {
-            if (STATS) ts.nodes++;
-            const BNode4& n = S.nodes[cur];
-            const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
-            const int4 ch = n.child;
-            bool h0, h1, h2, h3;
-            float t0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, inv, io, tmin, best, h0);
-            float t1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, inv, io, tmin, best, h1);
-            float t2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, inv, io, tmin, best, h2);
-            float t3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, inv, io, tmin, best, h3);
-            const float inf = __int_as_float(0x7f800000);
-            int c0 = (h0 && ch.x != kEmptyChild) ? ch.x : kEmptyChild;
-            int c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
-            int c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
-            int c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
-            t0 = c0 != kEmptyChild ? t0 : inf;
-            t1 = c1 != kEmptyChild ? t1 : inf;
-            t2 = c2 != kEmptyChild ? t2 : inf;
-            t3 = c3 != kEmptyChild ? t3 : inf;
-            // sort ascending (optimal 4-network); misses sink to the end with t = inf
-            cswap(t0, c0, t1, c1);
-            cswap(t2, c2, t3, c3);
-            cswap(t0, c0, t2, c2);
-            cswap(t1, c1, t3, c3);
-            cswap(t1, c1, t2, c2);
-            // push the farther hits (far first), continue with the nearest
-            if (c3 != kEmptyChild) push(c3);
-            if (c2 != kEmptyChild) push(c2);
-            if (c1 != kEmptyChild) push(c1);
-            if (c0 != kEmptyChild) {
-                cur = c0;
-                continue;
-            }
-        } else {
-            const int first = leaf_first(cur), cnt = leaf_count(cur);
-            for (int k = 0; k < cnt; ++k) {
-                const int ti = first + k;
-                if (STATS) ts.tris++;
-                const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
-                float t, u, v;
-                bool bk;
-                if (tri_intersect(A, E1, E2, o, d, tmin, best, t, u, v, bk)) {
-                    const int oi = __float_as_int(A.w);
-                    if (ANY) {
-                        h.tri = ti;
-                        h.orig = oi;
-                        return true;
-                    }
-                    if (t < best || oi < h.orig) {
-                        best = t; h.t = t; h.u = u; h.v = v; h.back = bk; h.tri = ti; h.orig = oi;
-                    }
+// ---- BVH4 traversal -----------------------------------------------------------------------
+// A per-lane state machine: one step is one inner node (4 slab tests, sorted push of the
+// far hits, descend) or one leaf (<= kLeafMax triangles).  traverse() loops it for one ray;
+// lane-refilling queue kernels (pt_wavefront.hip) interleave it with ray fetches.  Written
+// branch-reduced for 64-wide waves (PMC on the first version: ~16 % VALU lane utilisation,
+// SALU at 44 % of VALU from the per-push branches): the three pushes are unconditional
+// LDS stores with predicated stack-pointer increments and the triangle test is predicated
+// (same arithmetic and NaN behaviour as the oracle's tri_hit, without the early exits).
+// Closest hit is ordered by (t, original triangle index), so the result is independent of
+// BVH shape and visit order.
+struct TravState {
+    f3 o, d, inv, io;
+    float tmin, best;
+    int cur, sp, spc;  // current node/leaf, LDS stack depth, entries spilled
+    Hit h;
+};
+
+__device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, float tmax) {
+    s.o = o;
+    s.d = d;
+    s.inv = safe_inv(d);
+    s.io = mk(o.x * s.inv.x, o.y * s.inv.y, o.z * s.inv.z);
+    s.tmin = tmin;
+    s.best = tmax;
+    s.cur = 0;  // root (always an inner node)
+    s.sp = 0;
+    s.spc = 0;
+    s.h.tri = -1;
+    s.h.orig = 0x7fffffff;
+}
+
+// tri_intersect without early exits; accepts exactly the same (t, u, v).
+__device__ __forceinline__ bool tri_test(const float4 A, const float4 E1, const float4 E2, f3 o, f3 d, float tmin,
+                                         float tmax, float& th, float& uh, float& vh, bool& back) {
+    f3 v0 = mk(A.x, A.y, A.z), e1 = mk(E1.x, E1.y, E1.z), e2 = mk(E2.x, E2.y, E2.z);
+    f3 p = cross(d, e2);
+    float det = dot(e1, p);
+    float inv = 1.0f / det;
+    f3 tv = o - v0;
+    float u = dot(tv, p) * inv;
+    f3 q = cross(tv, e1);
+    float v = dot(d, q) * inv;
+    float t = dot(e2, q) * inv;
+    th = t;
+    uh = u;
+    vh = v;
+    back = det < 0.0f;
+    return (det != 0.0f) & !(u < 0.0f || u > 1.0f) & !(v < 0.0f || u + v > 1.0f) & (t >= tmin && t <= tmax);
+}
+
+// Move the bottom (DEPTH / 2) LDS entries to the spill array (rare).  With the spill full
+// (BVH4 deeper than ~30 levels, never produced for real scenes) the oldest half is dropped
+// and counted in TravStats::overflow.
+template <int DEPTH, bool STATS>
+__device__ __forceinline__ void stack_spill(TravState& s, int* __restrict__ stk, int stride, int* spill,
+                                         TravStats& ts) {
+    if (s.spc + (DEPTH / 2) <= kSpillDepth) {
+        for (int k = 0; k < (DEPTH / 2); ++k) spill[s.spc + k] = stk[k * stride];
+        s.spc += (DEPTH / 2);
+    } else if (STATS) {
+        ts.overflow++;
+    }
+    for (int k = (DEPTH / 2); k < s.sp; ++k) stk[(k - (DEPTH / 2)) * stride] = stk[k * stride];
+    s.sp -= (DEPTH / 2);
+}
+
+// LDS stack empty but entries spilled: bring the newest chunk back (rare).
+template <int DEPTH>
+__device__ __forceinline__ void stack_refill(TravState& s, int* __restrict__ stk, int stride, const int* spill) {
+    s.spc -= (DEPTH / 2);
+    for (int k = 0; k < (DEPTH / 2); ++k) stk[k * stride] = spill[s.spc + k];
+    s.sp = (DEPTH / 2);
+}
+
+// Returns true when the ray is finished.  `spill` holds stack entries beyond the LDS
+// depth (never reached on the benchmark scenes; see the overflow counter).
+template <bool ANY, bool STATS, int DEPTH>
+__device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
+                                          int* spill, TravStats& ts) {
+    if (s.cur >= 0) {
+        if (STATS) ts.nodes++;
+        const BNode4& n = S.nodes[s.cur];
+        const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
+        const int4 ch = n.child;
+        bool h0, h1, h2, h3;
+        float t0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, s.inv, s.io, s.tmin, s.best, h0);
+        float t1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, s.inv, s.io, s.tmin, s.best, h1);
+        float t2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, s.inv, s.io, s.tmin, s.best, h2);
+        float t3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, s.inv, s.io, s.tmin, s.best, h3);
+        const float inf = __int_as_float(0x7f800000);
+        int c0 = (h0 && ch.x != kEmptyChild) ? ch.x : kEmptyChild;
+        int c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
+        int c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
+        int c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
+        t0 = c0 != kEmptyChild ? t0 : inf;
+        t1 = c1 != kEmptyChild ? t1 : inf;
+        t2 = c2 != kEmptyChild ? t2 : inf;
+        t3 = c3 != kEmptyChild ? t3 : inf;
+        // sort ascending (optimal 4-network); misses sink to the end with t = inf
+        cswap(t0, c0, t1, c1);
+        cswap(t2, c2, t3, c3);
+        cswap(t0, c0, t2, c2);
+        cswap(t1, c1, t3, c3);
+        cswap(t1, c1, t2, c2);
+        // push the farther hits (far first), continue with the nearest
+        if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
+        {  // unconditional stores, predicated sp: an empty child's store lands in the slot
+           // the next valid one overwrites
+            int sp = s.sp;
+            stk[sp * stride] = c3;
+            sp += c3 != kEmptyChild;
+            stk[sp * stride] = c2;
+            sp += c2 != kEmptyChild;
+            stk[sp * stride] = c1;
+            sp += c1 != kEmptyChild;
+            s.sp = sp;
+        }
+        if (c0 != kEmptyChild) {
+            s.cur = c0;
+            return false;
+        }
+    } else {
+        const int first = leaf_first(s.cur), cnt = leaf_count(s.cur);
+        for (int k = 0; k < cnt; ++k) {
+            const int ti = first + k;
+            if (STATS) ts.tris++;
+            const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+            float t, u, v;
+            bool bk;
+#if PT_TRI_PREDICATED
+            const bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
+#else
+            const bool hit = tri_intersect(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
+#endif
+            const int oi = __float_as_int(A.w);
+            if (ANY) {
+                if (hit) {
+                    s.h.tri = ti;
+                    s.h.orig = oi;
+                    return true;
                 }
+            } else {
+                const bool take = hit && (t < s.best || oi < s.h.orig);
+                s.best = take ? t : s.best;
+                s.h.t = take ? t : s.h.t;
+                s.h.u = take ? u : s.h.u;
+                s.h.v = take ? v : s.h.v;
+                s.h.back = take ? bk : s.h.back;
+                s.h.tri = take ? ti : s.h.tri;
+                s.h.orig = take ? oi : s.h.orig;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        cur = sp < kStackDepth ? stk[sp * stride] : spill[sp - kStackDepth];
     }
-    return h.tri >= 0;
+    if (s.sp == 0) {
+        if (s.spc == 0) return true;
+        stack_refill<DEPTH>(s, stk, stride, spill);
+    }
+    --s.sp;
+    s.cur = stk[s.sp * stride];
+    return false;
+}
+
+// Whole traversal of one ray (megakernel, k_trace).
+template <bool ANY, bool STATS, int DEPTH>
+__device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h,
+                                         int* __restrict__ stk, int stride, TravStats& ts) {
+    if (STATS) ts.rays++;
+    TravState s;
+    trav_init(s, o, d, tmin, tmax);
+    if (S.ntri > 0) {
+        int spill[kSpillDepth];
+        while (!trav_step<ANY, STATS, DEPTH>(S, s, stk, stride, spill, ts)) {
+        }
+    }
+    h = s.h;
+    return s.h.tri >= 0;
 }
 
 // devicePrograms.cu:601-623 — pixel-centre primary ray.
@@ -297,11 +399,11 @@ __device__ __forceinline__ bool path_alive(const DevLaunch& L, const PathState& 
 
 // One iteration of SamplePath's loop: TraceRadiance + __closesthit__radiance
 // (devicePrograms.cu:343-514) or __miss__radiance (:576-583).  Returns false on a miss.
-template <int MODE, bool STATS>
+template <int MODE, bool STATS, int DEPTH>
 __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch& L, PathState& p, int* stk,
                                              int stride, TravStats& ts) {
     Hit h;
-    bool hit = traverse<false, STATS>(S, p.o, p.d, 0.0f, 100.0f, h, stk, stride, ts);
+    bool hit = traverse<false, STATS, DEPTH>(S, p.o, p.d, 0.0f, 100.0f, h, stk, stride, ts);
     if (!hit) {
         p.beta = mk(0, 0, 0);
         p.bounce = 100;
@@ -333,7 +435,7 @@ __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch&
         f3 ldn = normalize(ldir);
         f3 so = sf.pos + 1e-3f * sf.ng;
         Hit sh;
-        bool occluded = traverse<true, STATS>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
+        bool occluded = traverse<true, STATS, DEPTH>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
         f3 lds = to_local(sf.fr, ldn);
         if (!occluded) {
             f3 f = bsdf_f<MODE>(p.seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);

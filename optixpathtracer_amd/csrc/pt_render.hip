@@ -15,6 +15,11 @@ namespace pt {
 namespace {
 
 constexpr int kBlock = 256;
+// LDS traversal stack entries per lane (the megakernel is VGPR-limited, not LDS-limited).
+#ifndef PT_MK_STACK
+#define PT_MK_STACK 32
+#endif
+constexpr int kStack = PT_MK_STACK;
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
@@ -42,7 +47,7 @@ __device__ __forceinline__ void flush_stats(const DevLaunch& L, uint32_t segs, c
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) void k_render_mega(DevScene S, DevLaunch L) {
-    __shared__ int stack[kStackDepth * kBlock];
+    __shared__ int stack[kStack * kBlock];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -64,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void k_render_mega(DevScene S, DevLaunch L)
         path_start(p, co, cd, tea16(pix, L.frame_base));  // devicePrograms.cu:631
         while (true) {
             if (path_alive(L, p)) {
-                path_segment<MODE, STATS>(S, L, p, stk, kBlock, ts);
+                path_segment<MODE, STATS, kStack>(S, L, p, stk, kBlock, ts);
                 segs++;
                 continue;
             }
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void k_render_mega(DevScene S, DevLaunch L)
 
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays, int n, int* prim, float* th,
                                                   float* uh, float* vh, int* back, int any_hit) {
-    __shared__ int stack[kStackDepth * kBlock];
+    __shared__ int stack[kStack * kBlock];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* r = rays + 8 * (size_t)i;
@@ -91,8 +96,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays,
     Hit h;
     TravStats ts;
     int* stk = stack + threadIdx.x;
-    bool hit = any_hit ? traverse<true, false>(S, o, d, r[6], r[7], h, stk, kBlock, ts)
-                       : traverse<false, false>(S, o, d, r[6], r[7], h, stk, kBlock, ts);
+    bool hit = any_hit ? traverse<true, false, kStack>(S, o, d, r[6], r[7], h, stk, kBlock, ts)
+                       : traverse<false, false, kStack>(S, o, d, r[6], r[7], h, stk, kBlock, ts);
     prim[i] = hit ? h.orig : -1;
     th[i] = hit && !any_hit ? h.t : 0.0f;
     uh[i] = hit && !any_hit ? h.u : 0.0f;

@@ -23,6 +23,8 @@
 //
 // Every kernel reads queue lengths from device memory written by an earlier launch (kernel
 // boundaries order the hand-off), so a whole frame is enqueued without host round trips.
+#include <unordered_map>
+
 #include "pt_internal.h"
 
 namespace pt {
@@ -30,6 +32,12 @@ namespace pt {
 namespace {
 
 constexpr int kBlockWF = 256;
+// LDS traversal stack entries per lane: 16 KB per workgroup keeps the trace kernels
+// VGPR-limited rather than LDS-limited (deeper entries spill, see pt_device.h).
+#ifndef PT_WF_STACK
+#define PT_WF_STACK 16
+#endif
+constexpr int kStack = PT_WF_STACK;
 constexpr int kMissTri = -1;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -85,24 +93,68 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kQueue) = P;
 }
 
+// This wave's static slice of a queue of length n (grid sized to residency, so every wave
+// is resident and slices balance statistically; no fetch atomics).
+__device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
+    const int per = (n + nwaves - 1) / nwaves;
+    first = min(n, wave * per);
+    end = min(n, first + per);
+}
+
+// Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
+// for ray ri, `finish(ri, state)` consumes a finished ray.
+template <bool ANY, bool STATS, class Fetch, class Finish>
+__device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TravStats& ts, Fetch fetch,
+                                            Finish finish) {
+    int spill[kSpillDepth];
+    TravState st;
+    int next, end;
+    wave_slice(n, next, end);
+    int ri = -1;
+    while (true) {
+        const bool need = ri < 0;
+        const unsigned long long m = __ballot(need ? 1 : 0);
+        const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (need && next + pre < end) {
+            ri = next + pre;
+            fetch(ri, st);
+            if (STATS) ts.rays++;
+            if (S.ntri <= 0) {  // empty scene: no BVH root, every ray misses
+                finish(ri, st);
+                ri = -1;
+            }
+        }
+        next = min(next + __popcll(m), end);
+        if (!__any(ri >= 0 ? 1 : 0)) break;
+        if (ri >= 0 && trav_step<ANY, STATS, kStack>(S, st, stk, kBlockWF, spill, ts)) {
+            finish(ri, st);
+            ri = -1;
+        }
+    }
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(kBlockWF) void k_extend(DevScene S, WFState W, int b, unsigned long long* counters) {
-    __shared__ int stack[kStackDepth * kBlockWF];
+    __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    WF_LOOP(i, valid, n, cnt(W, b, kFetchExtend)) {
-        if (valid) {
-            const float4 a = ro[i], c = rd[i];
-            Hit h;
-            bool hit = traverse<false, STATS>(S, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f, h, stk,
-                                              kBlockWF, ts);
-            W.hit[i] = hit ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                           : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
-        }
-    }
+    trace_slice<false, STATS>(
+        S, n, stk, ts,
+        [&](int ri, TravState& st) {
+            const float4 a = ro[ri], c = rd[ri];
+            trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
+        },
+        [&](int ri, const TravState& st) {
+            const Hit& h = st.h;
+            W.hit[ri] = h.tri >= 0
+                            ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                            : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+        });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[0], (unsigned long long)n);
     if (STATS && counters) {
         unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
@@ -218,24 +270,24 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_fused(DevScene S, DevLaunch 
 }
 
 __global__ __launch_bounds__(kBlockWF) void k_shadow_add(DevScene S, WFState W, int b) {
-    __shared__ int stack[kStackDepth * kBlockWF];
+    __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    WF_LOOP(j, valid, n, cnt(W, b, kFetchShadow)) {
-        if (valid) {
+    trace_slice<true, false>(
+        S, n, stk, ts,
+        [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
-            Hit h;
-            bool occluded = traverse<true, false>(S, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w, h, stk,
-                                                  kBlockWF, ts);
-            if (!occluded) {
-                const int path = __float_as_int(a.w);
+            trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
+        },
+        [&](int j, const TravState& st) {
+            if (st.h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+                const int path = __float_as_int(W.sh_o[j].w);
                 const float4 k = W.sh_c[j];
                 float4 l = W.L[path];
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
-        }
-    }
+        });
 }
 
 template <int MODE>
@@ -281,19 +333,17 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_a(DevScene S, DevLaunch L, W
 }
 
 __global__ __launch_bounds__(kBlockWF) void k_shadow_vis(DevScene S, WFState W, int b) {
-    __shared__ int stack[kStackDepth * kBlockWF];
+    __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    WF_LOOP(j, valid, n, cnt(W, b, kFetchShadow)) {
-        if (valid) {
+    trace_slice<true, false>(
+        S, n, stk, ts,
+        [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
-            Hit h;
-            bool occluded = traverse<true, false>(S, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w, h, stk,
-                                                  kBlockWF, ts);
-            W.vis[__float_as_int(a.w)] = occluded ? 0 : 1;
-        }
-    }
+            trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
+        },
+        [&](int j, const TravState& st) { W.vis[__float_as_int(W.sh_o[j].w)] = st.h.tri >= 0 ? 0 : 1; });
 }
 
 template <int MODE>
@@ -365,11 +415,29 @@ __global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L) {
 
 inline bool fused_mode(int mode) { return mode == kModeLambert || mode == kModeConductor || mode == kModeDielectric; }
 
-// Grid covering `items` queue slots (one per thread).
+// Grid covering `items` queue slots (one per thread) — the shading kernels.
 template <typename K>
 dim3 resident_grid(K, int cus, int items) {
     (void)cus;
     return dim3((unsigned)std::max(1, (items + kBlockWF - 1) / kBlockWF));
+}
+
+// Exactly the blocks that are resident at once (occupancy query, cached) — the lane-
+// refilling trace kernels, whose waves each own a static queue slice.
+template <typename K>
+dim3 occupancy_grid(K kernel, int cus) {
+    static std::unordered_map<const void*, int> cache;
+    const void* key = reinterpret_cast<const void*>(kernel);
+    auto it = cache.find(key);
+    int per_cu = 0;
+    if (it == cache.end()) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockWF, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        cache[key] = per_cu;
+    } else {
+        per_cu = it->second;
+    }
+    return dim3((unsigned)(per_cu * std::max(1, cus)));
 }
 
 template <int MODE>
@@ -451,18 +519,18 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     const bool fused = fused_mode(mode);
     for (int b = 0; b < maxb; ++b) {
         if (stats)
-            hipLaunchKernelGGL(k_extend<true>, resident_grid(k_extend<true>, cus, P), dim3(kBlockWF), 0, stream, S, W,
+            hipLaunchKernelGGL(k_extend<true>, occupancy_grid(k_extend<true>, cus), dim3(kBlockWF), 0, stream, S, W,
                                b, L.counters);
         else
-            hipLaunchKernelGGL(k_extend<false>, resident_grid(k_extend<false>, cus, P), dim3(kBlockWF), 0, stream, S,
+            hipLaunchKernelGGL(k_extend<false>, occupancy_grid(k_extend<false>, cus), dim3(kBlockWF), 0, stream, S,
                                W, b, L.counters);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (fused) {
             if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_shadow_add, resident_grid(k_shadow_add, cus, P), dim3(kBlockWF), 0, stream, S, W, b);
+            hipLaunchKernelGGL(k_shadow_add, occupancy_grid(k_shadow_add, cus), dim3(kBlockWF), 0, stream, S, W, b);
         } else {
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_shadow_vis, resident_grid(k_shadow_vis, cus, P), dim3(kBlockWF), 0, stream, S, W, b);
+            hipLaunchKernelGGL(k_shadow_vis, occupancy_grid(k_shadow_vis, cus), dim3(kBlockWF), 0, stream, S, W, b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 1)) != hipSuccess) return e;
         }
