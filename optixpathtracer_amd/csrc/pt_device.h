@@ -67,32 +67,6 @@ struct TravStats {
     uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0;
 };
 
-// Moller-Trumbore; OptiX barycentric convention (u weights v1, v weights v2); closed
-// interval [tmin, tmax]; det < 0 <=> back face (ray along the CCW normal).  Same
-// arithmetic order as the oracle's tri_hit (edges precomputed with the same subtraction).
-__device__ __forceinline__ bool tri_intersect(const float4 A, const float4 E1, const float4 E2, f3 o, f3 d,
-                                              float tmin, float tmax, float& th, float& uh, float& vh,
-                                              bool& back) {
-    f3 v0 = mk(A.x, A.y, A.z), e1 = mk(E1.x, E1.y, E1.z), e2 = mk(E2.x, E2.y, E2.z);
-    f3 p = cross(d, e2);
-    float det = dot(e1, p);
-    if (det == 0.0f) return false;
-    float inv = 1.0f / det;
-    f3 tv = o - v0;
-    float u = dot(tv, p) * inv;
-    if (u < 0.0f || u > 1.0f) return false;
-    f3 q = cross(tv, e1);
-    float v = dot(d, q) * inv;
-    if (v < 0.0f || u + v > 1.0f) return false;
-    float t = dot(e2, q) * inv;
-    if (!(t >= tmin && t <= tmax)) return false;
-    th = t;
-    uh = u;
-    vh = v;
-    back = det < 0.0f;
-    return true;
-}
-
 // Reciprocal direction; zero components map to a huge finite value so the fma slab form
 // never produces 0*inf.
 __device__ __forceinline__ f3 safe_inv(f3 d) {
@@ -130,8 +104,8 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
 // The LDS depth is a template parameter (DEPTH): it trades LDS per workgroup against
 // occupancy per kernel (see pt_render.hip / pt_wavefront.hip).
 constexpr int kSpillDepth = 64;  // spill + LDS hold a BVH4 path of depth > 20
-#ifndef PT_TRI_PREDICATED
-#define PT_TRI_PREDICATED 1
+#ifndef PT_TRI_PER_STEP
+#define PT_TRI_PER_STEP 1
 #endif
 
 // ---- BVH4 traversal -----------------------------------------------------------------------
@@ -165,7 +139,10 @@ __device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, 
     s.h.orig = 0x7fffffff;
 }
 
-// tri_intersect without early exits; accepts exactly the same (t, u, v).
+// Moller-Trumbore; OptiX barycentric convention (u weights v1, v weights v2); closed
+// interval [tmin, tmax]; det < 0 <=> back face (ray along the CCW normal).  Same
+// arithmetic order and NaN behaviour as the oracle's tri_hit (edges precomputed with the
+// same subtraction); predicated instead of early exits (no divergent branches per test).
 __device__ __forceinline__ bool tri_test(const float4 A, const float4 E1, const float4 E2, f3 o, f3 d, float tmin,
                                          float tmax, float& th, float& uh, float& vh, bool& back) {
     f3 v0 = mk(A.x, A.y, A.z), e1 = mk(E1.x, E1.y, E1.z), e2 = mk(E2.x, E2.y, E2.z);
@@ -257,17 +234,20 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         }
     } else {
         const int first = leaf_first(s.cur), cnt = leaf_count(s.cur);
+#if PT_TRI_PER_STEP
+        // one triangle per step: a lane in a leaf costs the wave one triangle test per
+        // iteration instead of holding node lanes for the whole leaf
+        const int ti = first;
+        {
+#else
         for (int k = 0; k < cnt; ++k) {
             const int ti = first + k;
+#endif
             if (STATS) ts.tris++;
             const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
             float t, u, v;
             bool bk;
-#if PT_TRI_PREDICATED
             const bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
-#else
-            const bool hit = tri_intersect(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
-#endif
             const int oi = __float_as_int(A.w);
             if (ANY) {
                 if (hit) {
@@ -286,6 +266,12 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
                 s.h.orig = take ? oi : s.h.orig;
             }
         }
+#if PT_TRI_PER_STEP
+        if (cnt > 1) {
+            s.cur = ~(((first + 1) << 3) | (cnt - 2));  // rest of the leaf
+            return false;
+        }
+#endif
     }
     if (s.sp == 0) {
         if (s.spc == 0) return true;

@@ -20,6 +20,10 @@ constexpr int kBlock = 256;
 #define PT_MK_STACK 32
 #endif
 constexpr int kStack = PT_MK_STACK;
+// Minimum waves per SIMD the register allocator must allow (caps VGPRs at 512/N).
+#ifndef PT_MK_WAVES
+#define PT_MK_WAVES 1
+#endif
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
@@ -46,7 +50,7 @@ __device__ __forceinline__ void flush_stats(const DevLaunch& L, uint32_t segs, c
 }
 
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(kBlock) void k_render_mega(DevScene S, DevLaunch L) {
+__global__ __launch_bounds__(kBlock, PT_MK_WAVES) void k_render_mega(DevScene S, DevLaunch L) {
     __shared__ int stack[kStack * kBlock];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;

@@ -38,24 +38,12 @@ constexpr int kBlockWF = 256;
 #define PT_WF_STACK 16
 #endif
 constexpr int kStack = PT_WF_STACK;
+#ifndef PT_WF_WAVES
+#define PT_WF_WAVES 1
+#endif
 constexpr int kMissTri = -1;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-
-// Wave-wide compaction: every active lane of the wave calls this (converged); lanes with
-// pred get consecutive slots.  One atomic per wave.
-__device__ __forceinline__ int wave_append(int* counter, bool pred) {
-    const unsigned long long m = __ballot(pred ? 1 : 0);
-    const int cnt = __popcll(m);
-    int base = 0;
-    if (cnt > 0) {
-        const int leader = __ffsll((unsigned long long)m) - 1;
-        if (lane_id() == leader) base = atomicAdd(counter, cnt);
-        base = __shfl(base, leader, 64);
-    }
-    const int prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    return base + prefix;
-}
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -63,20 +51,45 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
     return v;
 }
 
-// Per-bounce counter block (kCnt ints): queue length, shadow-queue length, and one
-// work-fetch head per kernel of the bounce (zeroed by the per-frame memset).
-constexpr int kCnt = 8;
-enum { kQueue = 0, kShadowQ = 1, kFetchExtend = 2, kFetchShade = 3, kFetchShadow = 4, kFetchShadeB = 5 };
-__device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + kCnt * b + k; }
+// Per-bounce counters: queue length and shadow-queue length, each on its own 128-B line
+// (appends from different queues never contend for one L2 line).  Zeroed per frame.
+constexpr int kCnt = 2;
+constexpr int kCntStride = 32;  // ints per counter = 128 B
+enum { kQueue = 0, kShadowQ = 1 };
+__device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
+inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * kCnt * (size_t)(max_bounces + 2); }
 
-// Work distribution: one queue item per thread over a grid sized to the queue capacity;
-// waves past the live queue length exit at once and the hardware dispatcher balances the
-// divergent rest.  (Measured alternatives, see DESIGN.md: persistent grids with one atomic
-// fetch head per kernel serialise on the head — MI355X_MICROARCH.md "dequeue" — and
-// chunked fetching starves waves.)
-#define WF_LOOP(i, valid, n, head)                                                                   \
-    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x), valid = (i < (n)), i##_once = 1;       \
-         i##_once && __any(valid); i##_once = 0)
+// Shading kernels: 1024-thread blocks, one queue item per thread over a grid sized to the
+// queue capacity; blocks past the live queue length exit at once.  Queue appends are
+// aggregated per block (one atomic per 1024 items): same-address atomics serialise at the
+// L2 (≈90 per µs per word, MI355X_MICROARCH.md "dequeue"), and one atomic per wave cost
+// ≈0.4 ms per shading launch at 2 M paths.  (Measured alternatives, see DESIGN.md:
+// persistent grids with one atomic fetch head serialise the same way, and chunked fetching
+// starves waves.)
+constexpr int kBlockSh = 1024;
+constexpr int kWavesSh = kBlockSh / 64;
+
+// Block-wide compaction: every thread of the block calls this (uniform control flow);
+// threads with pred get consecutive slots.  `lds` is kWavesSh + 1 ints of shared memory
+// private to this call site.
+__device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
+    const unsigned long long m = __ballot(pred ? 1 : 0);
+    const int prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const int wave = threadIdx.x >> 6;
+    if (lane_id() == 0) lds[wave] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kWavesSh; ++w) {
+            const int c = lds[w];
+            lds[w] = tot;
+            tot += c;
+        }
+        lds[kWavesSh] = tot > 0 ? atomicAdd(counter, tot) : 0;
+    }
+    __syncthreads();
+    return lds[kWavesSh] + lds[wave] + prefix;
+}
 
 __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame) {
     const int P = L.width * L.height;
@@ -136,7 +149,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(kBlockWF) void k_extend(DevScene S, WFState W, int b, unsigned long long* counters) {
+__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WFState W, int b, unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
@@ -203,13 +216,17 @@ __device__ __forceinline__ bool continue_path(const SurfaceHit& sf, const BSampl
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBlockWF) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
-    WF_LOOP(i, valid, n, cnt(W, b, kFetchShade)) {
+    __shared__ int lds_sh[kWavesSh + 1], lds_q[kWavesSh + 1];
+    if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
+    {
+        const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+        const bool valid = i < n;
         bool emit_shadow = false, emit_next = false;
         f3 so, sdir, contrib, o, d;
         float stmax = 0.0f;
@@ -255,13 +272,13 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_fused(DevScene S, DevLaunch 
                 }
             }
         }
-        const int si = wave_append(cnt(W, b, kShadowQ), emit_shadow);
+        const int si = block_append(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
         if (emit_shadow) {
             W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(path));
             W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
             W.sh_c[si] = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
         }
-        const int qi = wave_append(cnt(W, b + 1, kQueue), emit_next);
+        const int qi = block_append(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
             nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -269,7 +286,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_fused(DevScene S, DevLaunch 
     }
 }
 
-__global__ __launch_bounds__(kBlockWF) void k_shadow_add(DevScene S, WFState W, int b) {
+__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_add(DevScene S, WFState W, int b) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
     int* stk = stack + threadIdx.x;
@@ -291,11 +308,15 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow_add(DevScene S, WFState W, 
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBlockWF) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
-    WF_LOOP(i, valid, n, cnt(W, b, kFetchShade)) {
+    __shared__ int lds_sh[kWavesSh + 1];
+    if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
+    {
+        const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+        const bool valid = i < n;
         bool emit = false;
         f3 so, sdir;
         float stmax = 0.0f;
@@ -324,7 +345,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_a(DevScene S, DevLaunch L, W
                 }
             }
         }
-        const int si = wave_append(cnt(W, b, kShadowQ), emit);
+        const int si = block_append(cnt(W, b, kShadowQ), emit, lds_sh);
         if (emit) {
             W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(path));
             W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
@@ -332,7 +353,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_a(DevScene S, DevLaunch L, W
     }
 }
 
-__global__ __launch_bounds__(kBlockWF) void k_shadow_vis(DevScene S, WFState W, int b) {
+__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S, WFState W, int b) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
     int* stk = stack + threadIdx.x;
@@ -347,13 +368,17 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow_vis(DevScene S, WFState W, 
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBlockWF) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockSh) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
-    WF_LOOP(i, valid, n, cnt(W, b, kFetchShadeB)) {
+    __shared__ int lds_q[kWavesSh + 1];
+    if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
+    {
+        const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+        const bool valid = i < n;
         bool emit_next = false;
         f3 o, d;
         int path = 0;
@@ -394,7 +419,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shade_b(DevScene S, DevLaunch L, W
                 }
             }
         }
-        const int qi = wave_append(cnt(W, b + 1, kQueue), emit_next);
+        const int qi = block_append(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
             nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -415,12 +440,8 @@ __global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L) {
 
 inline bool fused_mode(int mode) { return mode == kModeLambert || mode == kModeConductor || mode == kModeDielectric; }
 
-// Grid covering `items` queue slots (one per thread) — the shading kernels.
-template <typename K>
-dim3 resident_grid(K, int cus, int items) {
-    (void)cus;
-    return dim3((unsigned)std::max(1, (items + kBlockWF - 1) / kBlockWF));
-}
+// Grid covering `items` slots, one per thread.
+inline dim3 item_grid(int items, int block) { return dim3((unsigned)std::max(1, (items + block - 1) / block)); }
 
 // Exactly the blocks that are resident at once (occupancy query, cached) — the lane-
 // refilling trace kernels, whose waves each own a static queue slice.
@@ -445,13 +466,13 @@ hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const
                         int items, hipStream_t stream, int phase) {
     if (fused) {
         if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
-            hipLaunchKernelGGL((k_shade_fused<MODE>), resident_grid(k_shade_fused<MODE>, cus, items), dim3(kBlockWF),
+            hipLaunchKernelGGL((k_shade_fused<MODE>), item_grid(items, kBlockSh), dim3(kBlockSh),
                                0, stream, S, L, W, b);
     } else if (phase == 0) {
-        hipLaunchKernelGGL((k_shade_a<MODE>), resident_grid(k_shade_a<MODE>, cus, items), dim3(kBlockWF), 0, stream,
+        hipLaunchKernelGGL((k_shade_a<MODE>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream,
                            S, L, W, b);
     } else {
-        hipLaunchKernelGGL((k_shade_b<MODE>), resident_grid(k_shade_b<MODE>, cus, items), dim3(kBlockWF), 0, stream,
+        hipLaunchKernelGGL((k_shade_b<MODE>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream,
                            S, L, W, b);
     }
     return hipGetLastError();
@@ -473,7 +494,7 @@ hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevL
 size_t wavefront_bytes(int paths, int max_bounces) {
     size_t P = (size_t)paths;
     return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 2 /*beta, L*/ + 3 /*shadow*/) +
-           P * 2 * sizeof(int) + sizeof(int) * kCnt * (size_t)(max_bounces + 2);
+           P * 2 * sizeof(int) + count_bytes(max_bounces);
 }
 
 hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
@@ -494,7 +515,7 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
     al((void**)&W.sh_c, P * sizeof(float4));
     al((void**)&W.aux, P * sizeof(int));
     al((void**)&W.vis, P * sizeof(int));
-    al((void**)&W.count, sizeof(int) * kCnt * (size_t)(max_bounces + 2));
+    al((void**)&W.count, count_bytes(max_bounces));
     W.paths = paths;
     W.max_bounces = max_bounces;
     return e;
@@ -512,9 +533,9 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
                                   uint32_t frame, int cus, hipStream_t stream) {
     const int P = L.width * L.height;
     const int maxb = L.max_bounces;
-    hipError_t e = hipMemsetAsync(W.count, 0, sizeof(int) * kCnt * (size_t)(maxb + 2), stream);
+    hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_camera, resident_grid(k_camera, cus, P), dim3(kBlockWF), 0, stream, W, L, frame);
+    hipLaunchKernelGGL(k_camera, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L, frame);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const bool fused = fused_mode(mode);
     for (int b = 0; b < maxb; ++b) {
@@ -536,7 +557,7 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_accum, resident_grid(k_accum, cus, P), dim3(kBlockWF), 0, stream, W, L);
+    hipLaunchKernelGGL(k_accum, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L);
     return hipGetLastError();
 }
 

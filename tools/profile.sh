@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round profile on the GPU box (repo root): bench JSON, rocprofv3 kernel-trace stats of the
+# same bench command, PMC traffic passes (FETCH_SIZE / WRITE_SIZE in separate runs, as
+# MI355X_MICROARCH.md prescribes) and profiles/traffic.json for bench.py's roofline.traffic.
+#   tools/profile.sh TAG [bench args...]
+set -e
+TAG=${1:-r01}; shift || true
+ARGS="$@"
+ROOT="$GRAFT_REPO_ROOT"; [ -z "$ROOT" ] && ROOT=$(pwd)
+OUT="$ROOT/gpurun_out/prof_$TAG"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+cd "$ROOT"
+echo "[profile] kernel trace"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
+echo "[profile] FETCH_SIZE"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline $ARGS > "$OUT/fetch.json" 2> "$OUT/fetch.log"
+echo "[profile] WRITE_SIZE"
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline $ARGS > "$OUT/write.json" 2> "$OUT/write.log"
+python3 tools/traffic.py "$OUT" > "$OUT/traffic.json"
+cat "$OUT/traffic.json"
+echo "[profile] done"

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the dominant render kernel from rocprofv3 PMC passes.
+
+    python tools/traffic.py PROFILE_DIR   (written by tools/profile.sh)
+
+FETCH_SIZE and WRITE_SIZE come from separate rocprofv3 runs.  Both are in KiB.  On gfx950
+FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled here.  WRITE_SIZE
+is exact for 16-B-per-lane stores.  These corrections follow MI355X_MICROARCH.md §HBM.  The
+result is written to profiles/traffic.json, where bench.py reads it for `roofline.traffic`.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import sys
+from pathlib import Path
+
+KERNELS = ("k_render_mega", "k_extend")  # dominant kernel of the megakernel / wavefront path
+
+
+def counter_rows(d: Path):
+    for f in sorted(d.rglob("*counter_collection.csv")):
+        with open(f) as fh:
+            yield from csv.DictReader(fh)
+
+
+def per_kernel(d: Path, counter: str):
+    vals: dict[str, list[float]] = {}
+    for row in counter_rows(d):
+        if row.get("Counter_Name") != counter:
+            continue
+        name = row["Kernel_Name"]
+        for k in KERNELS:
+            if k in name:
+                vals.setdefault(k, []).append(float(row["Counter_Value"]))
+    return vals
+
+
+def kernel_stats(d: Path):
+    out = {}
+    for f in sorted(d.rglob("*kernel_stats.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                for k in KERNELS:
+                    if k in row["Name"]:
+                        out[k] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                                  "total_ns": float(row["TotalDurationNs"])}
+    return out
+
+
+def main():
+    root = Path(sys.argv[1])
+    fetch = per_kernel(root / "fetch", "FETCH_SIZE")
+    write = per_kernel(root / "write", "WRITE_SIZE")
+    stats = kernel_stats(root / "kt")
+    kernel = next((k for k in KERNELS if k in fetch and k in write), None)
+    if kernel is None:
+        print(json.dumps({"error": "no PMC rows for the render kernels"}))
+        return
+    f_kib = sum(fetch[kernel]) / len(fetch[kernel])
+    w_kib = sum(write[kernel]) / len(write[kernel])
+    hbm = 2.0 * f_kib * 1024.0 + w_kib * 1024.0
+    print(json.dumps({
+        "kernel": kernel,
+        "dispatches": len(fetch[kernel]),
+        "fetch_size_kib_mean": round(f_kib, 3),
+        "write_size_kib_mean": round(w_kib, 3),
+        "hbm_bytes_per_launch": int(hbm),
+        "kernel_trace": stats.get(kernel),
+        "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes",
+    }, indent=1))
+
+
+if __name__ == "__main__":
+    main()
