@@ -33,6 +33,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 BYTES_PER_SEGMENT = 396  # compulsory SoA queue + gather traffic per path segment
 BYTES_PER_SAMPLE = 12  # final fp32 RGB accumulate
+BYTES_PER_TRACE = 48  # k_extend share of the segment bytes: ray read 32 B + hit write 16 B
 
 
 def log(*a):
@@ -68,13 +69,11 @@ def cpu_baseline(scene, args, budget_s: float):
     o = OracleScene(scene)
     lp = o.launch(args.width, args.height, args.depth)
     y0 = args.height // 2
-    # calibration band: 2 rows x 1 spp
+    rows = args.height - y0  # the lower half of the frame, 1 spp, as the calibration pass
     t = time.perf_counter()
-    o.render(lp, 1, 1, rect=(0, y0, args.width, y0 + 2), threads=threads)
-    dt = max(time.perf_counter() - t, 1e-3)
-    per_row = dt / 2
-    rows = int(max(2, min(args.height - y0, budget_s / per_row)))
-    spp = int(max(1, min(args.spp, budget_s / (per_row * rows))))
+    o.render(lp, 1, 1, rect=(0, y0, args.width, y0 + rows), threads=threads)
+    per_spp = max(time.perf_counter() - t, 1e-3)
+    spp = int(max(1, min(args.spp, budget_s / per_spp)))
     t = time.perf_counter()
     _, segs = o.render(lp, 1, spp, rect=(0, y0, args.width, y0 + rows), threads=threads)
     dt = time.perf_counter() - t
@@ -114,6 +113,8 @@ def main():
     t0 = time.perf_counter()
     r = setup_renderer(scene, args.width, args.height, args.depth, device=local_rank, kernel=args.kernel)
     r.set_frames_per_launch(args.frames_per_launch)
+    if args.kernel != 0:  # wavefront (auto resolves to it): time every k_extend launch
+        r.set_kernel_timing(True)
     setup_s = time.perf_counter() - t0
     bvh_ms = r.stats()["bvh_build_ms"]
     dev = torch.device("cuda", local_rank)
@@ -162,17 +163,30 @@ def main():
     if rank == 0:
         img = accum.cpu().numpy()
         nan_px = int(np.isnan(img).any(axis=-1).sum())
-        launches = max(1, int(st["kernel_launches"]))
         kernel_s = st["total_render_ms"] / 1e3
         alg_bytes = st["segments"] * BYTES_PER_SEGMENT + st["samples"] * BYTES_PER_SAMPLE
-        per_launch_bytes = alg_bytes / launches
-        avg_launch_s = kernel_s / launches
+        if st["trace_kernel_launches"] > 0:
+            # wavefront: the dominant kernel is the closest-hit trace k_extend (one launch per
+            # bounce), each launch bracketed by its own HIP event pair on the library stream
+            dom = "k_extend"
+            launches = int(st["trace_kernel_launches"])
+            per_launch_bytes = st["segments"] * BYTES_PER_TRACE / launches
+            avg_launch_s = st["trace_kernel_ms"] / 1e3 / launches
+            bytes_def = "48 B per traced segment (ray read 32 + hit write 16)"
+        else:
+            dom = "k_render_mega"
+            launches = max(1, int(st["kernel_launches"]))
+            per_launch_bytes = alg_bytes / launches
+            avg_launch_s = kernel_s / launches
+            bytes_def = "396 B per segment + 12 B per sample"
         achieved = per_launch_bytes / avg_launch_s / 1e9
         traffic = None
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
-                traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
+                tjd = json.loads(tj.read_text())
+                if tjd.get("kernel") == dom:
+                    traffic = tjd.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         out = {
@@ -198,7 +212,7 @@ def main():
                 "spp_per_gpu_per_step": args.spp,
                 "max_depth": args.depth,
                 "material_mode": "lambert" if scene.material_mode == 1 else str(scene.material_mode),
-                "kernel": {0: "megakernel", 1: "wavefront", 2: "auto"}[args.kernel],
+                "kernel": {0: "megakernel", 1: "wavefront", 2: "auto (wavefront)"}[args.kernel],
                 "frames_per_launch": args.frames_per_launch,
                 "parallelism": f"spp-shard x{world}",
                 "lbvh_build_ms": round(bvh_ms, 3),
@@ -210,11 +224,14 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic,
-                "kernel": "k_render_mega",
+                "kernel": dom,
                 "bytes_per_launch": int(per_launch_bytes),
-                "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "bytes_def": bytes_def,
+                "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "launches": launches,
                 "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
+                # SURVEY.md §8(d) whole-path figure: (segments*396 + samples*12) / render time
+                "pipeline_gbps": round(alg_bytes / max(kernel_s, 1e-9) / 1e9, 2),
             },
             "image": {"mean": float(np.nanmean(img) / (args.spp * world)), "nan_pixels": nan_px},
         }

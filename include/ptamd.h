@@ -35,7 +35,7 @@ extern "C" {
 /* Render-kernel variants (all produce the same image). */
 #define PT_KERNEL_MEGA 0      /* one thread per pixel, frames looped in registers */
 #define PT_KERNEL_WAVEFRONT 1 /* wavefront: per-bounce kernels over SoA ray/hit queues, wave compaction */
-#define PT_KERNEL_AUTO 2      /* the faster of the two per material mode (measured) */
+#define PT_KERNEL_AUTO 2      /* the faster path (measured): currently the wavefront in every mode */
 
 /* Mesh: ModelLoading/Mesh.h:9-45 (vertecies, normal, texCoord, index, ModelMatrix, albedo,
  * metallic, roughness, texture ids).  Borrowed only during pt_create (deep copy). */
@@ -101,6 +101,10 @@ typedef struct pt_stats {
     uint64_t tri_tests;
     uint64_t rays;
     uint64_t stack_overflows;
+    /* closest-hit trace kernel of the wavefront path (k_extend), only timed while
+       pt_set_kernel_timing(r, 1): summed per-launch HIP-event time and launch count */
+    double trace_kernel_ms;
+    uint64_t trace_kernel_launches;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -127,6 +131,9 @@ int pt_set_kernel(pt_renderer* r, int32_t kernel);
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames);
 /* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */
 int pt_set_traversal_stats(pt_renderer* r, int32_t enable);
+/* Bracket every wavefront closest-hit trace launch (k_extend) with its own HIP event pair
+ * on the library stream (pt_stats.trace_kernel_ms / trace_kernel_launches).  Off by default. */
+int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
 
 /* OptixRenderer::Render(glm::vec3 h_pixels[]) — OptixRenderer.cpp:617-647: frame.id++,
  * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before

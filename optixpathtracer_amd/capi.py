@@ -90,6 +90,8 @@ class pt_stats(C.Structure):
         ("tri_tests", C.c_uint64),
         ("rays", C.c_uint64),
         ("stack_overflows", C.c_uint64),
+        ("trace_kernel_ms", C.c_double),
+        ("trace_kernel_launches", C.c_uint64),
     ]
 
 
@@ -109,6 +111,7 @@ SIGNATURES = {
     "pt_set_kernel": (C.c_int, [_R, C.c_int32]),
     "pt_set_frames_per_launch": (C.c_int, [_R, C.c_int32]),
     "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
+    "pt_set_kernel_timing": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),
     "pt_accum_clear": (C.c_int, [_R]),
     "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),

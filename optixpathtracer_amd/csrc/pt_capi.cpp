@@ -40,6 +40,46 @@ int hip_fail(hipError_t e, const char* where) {
 // glm mat4 * vec4 for the host-side pre-transform (GetVertices, devicePrograms.cu:77-81)
 void xform4(const float* m, const float v[4], float out[4]) { mat4_mul_vec4(m, v, out); }
 
+// Reusable HIP event pairs, one pair per timed launch; summed once the launches retire.
+struct EventPool {
+    std::vector<hipEvent_t> start, stop;
+    size_t used = 0;
+    hipError_t next(hipEvent_t* a, hipEvent_t* b) {
+        if (used == start.size()) {
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            hipError_t e = hipEventCreate(&e0);
+            if (e == hipSuccess) e = hipEventCreate(&e1);
+            if (e != hipSuccess) return e;
+            start.push_back(e0);
+            stop.push_back(e1);
+        }
+        *a = start[used];
+        *b = stop[used];
+        used++;
+        return hipSuccess;
+    }
+    hipError_t collect(double* ms_sum, size_t* n) {
+        *ms_sum = 0.0;
+        *n = used;
+        if (used == 0) return hipSuccess;
+        hipError_t e = hipEventSynchronize(stop[used - 1]);
+        for (size_t i = 0; i < used && e == hipSuccess; ++i) {
+            float ms = 0.0f;
+            e = hipEventElapsedTime(&ms, start[i], stop[i]);
+            *ms_sum += ms;
+        }
+        used = 0;
+        return e;
+    }
+    void destroy() {
+        for (hipEvent_t e : start) (void)hipEventDestroy(e);
+        for (hipEvent_t e : stop) (void)hipEventDestroy(e);
+        start.clear();
+        stop.clear();
+        used = 0;
+    }
+};
+
 }  // namespace
 
 struct pt_renderer {
@@ -73,9 +113,14 @@ struct pt_renderer {
     float* user_accum = nullptr;
     unsigned long long* d_counters = nullptr;
     // stats: one HIP event pair per kernel launch, on the library stream
-    std::vector<hipEvent_t> ev_start, ev_stop;
-    size_t ev_used = 0;
+    EventPool ev;
     uint64_t launches = 0;
+    // optional per-launch timing of the wavefront's closest-hit trace kernel (k_extend)
+    bool kernel_timing = false;
+    EventPool tev;
+    std::vector<hipEvent_t> tev_frame;  // 2 * max_bounces events handed to one frame
+    double trace_ms = 0.0;
+    uint64_t trace_launches = 0;
     bool pending = false;
     uint64_t samples = 0;
     double last_ms = 0.0, total_ms = 0.0;
@@ -99,32 +144,21 @@ namespace {
 
 int collect_pending(pt_renderer* r) {
     if (!r->pending) return PT_OK;
-    double sum = 0.0;
-    if (r->ev_used > 0) PT_HIP(hipEventSynchronize(r->ev_stop[r->ev_used - 1]), "hipEventSynchronize");
-    for (size_t i = 0; i < r->ev_used; ++i) {
-        float ms = 0.0f;
-        PT_HIP(hipEventElapsedTime(&ms, r->ev_start[i], r->ev_stop[i]), "hipEventElapsedTime");
-        sum += ms;
-    }
-    r->launches += r->ev_used;
-    r->ev_used = 0;
+    double sum = 0.0, tsum = 0.0;
+    size_t n = 0, tn = 0;
+    PT_HIP(r->ev.collect(&sum, &n), "frame events");
+    PT_HIP(r->tev.collect(&tsum, &tn), "trace-kernel events");
+    r->launches += n;
     r->last_ms = sum;
     r->total_ms += sum;
+    r->trace_ms += tsum;
+    r->trace_launches += tn;
     r->pending = false;
     return PT_OK;
 }
 
 int next_event_pair(pt_renderer* r, hipEvent_t* a, hipEvent_t* b) {
-    if (r->ev_used == r->ev_start.size()) {
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        PT_HIP(hipEventCreate(&e0), "hipEventCreate");
-        PT_HIP(hipEventCreate(&e1), "hipEventCreate");
-        r->ev_start.push_back(e0);
-        r->ev_stop.push_back(e1);
-    }
-    *a = r->ev_start[r->ev_used];
-    *b = r->ev_stop[r->ev_used];
-    r->ev_used++;
+    PT_HIP(r->ev.next(a, b), "hipEventCreate");
     return PT_OK;
 }
 
@@ -153,13 +187,11 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
     r->pending = true;
-    // AUTO: the megakernel wins where the BRDF eval has no RNG side effects (Lambert,
-    // Conductor, Dielectric: short, uniform shading); the wavefront wins on Default/Layered,
-    // whose random-walk BSDF would otherwise stall the traversal waves.
+    // AUTO = wavefront: it beats the megakernel in every material mode (1080p
+    // depth 8 Msamples/s, wavefront / megakernel: Lambert 389/288, Conductor 390/260,
+    // Dielectric 566/492, Layered 179/92, Default 179/53).
     int kernel = r->kernel;
-    if (kernel == PT_KERNEL_AUTO)
-        kernel = (r->material_mode == PT_MAT_DEFAULT || r->material_mode == PT_MAT_LAYERED) ? PT_KERNEL_WAVEFRONT
-                                                                                            : PT_KERNEL_MEGA;
+    if (kernel == PT_KERNEL_AUTO) kernel = PT_KERNEL_WAVEFRONT;
     if (kernel == PT_KERNEL_WAVEFRONT) {
         const int P = r->width * r->height;
         if (r->wf.paths != P || r->wf.max_bounces < r->max_bounces) {
@@ -174,9 +206,16 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
             hipEvent_t a, b;
             rc = next_event_pair(r, &a, &b);
             if (rc) return rc;
+            const hipEvent_t* tev = nullptr;
+            if (r->kernel_timing) {
+                r->tev_frame.resize(2 * (size_t)r->max_bounces);
+                for (int k = 0; k < r->max_bounces; ++k)
+                    PT_HIP(r->tev.next(&r->tev_frame[2 * k], &r->tev_frame[2 * k + 1]), "hipEventCreate");
+                tev = r->tev_frame.data();
+            }
             PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
             PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, dev_cus,
-                                          r->stream),
+                                          r->stream, tev),
                    "wavefront launch");
             PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
         }
@@ -353,8 +392,8 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_counters) (void)hipFree(r->d_counters);
     wavefront_free(r->wf);
-    for (hipEvent_t e : r->ev_start) (void)hipEventDestroy(e);
-    for (hipEvent_t e : r->ev_stop) (void)hipEventDestroy(e);
+    r->ev.destroy();
+    r->tev.destroy();
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
     return PT_OK;
@@ -521,6 +560,8 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->rays = c[3];
     out->stack_overflows = c[4];
     out->triangles = r->ntri;
+    out->trace_kernel_ms = r->trace_ms;
+    out->trace_kernel_launches = r->trace_launches;
     return PT_OK;
 }
 
@@ -533,6 +574,8 @@ int pt_stats_reset(pt_renderer* r) {
     r->last_ms = r->total_ms = 0.0;
     r->calls = 0;
     r->launches = 0;
+    r->trace_ms = 0.0;
+    r->trace_launches = 0;
     return PT_OK;
 }
 
@@ -656,5 +699,13 @@ int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* pr
 extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_traversal_stats: NULL");
     r->trav_stats = enable != 0;
+    return PT_OK;
+}
+
+extern "C" int pt_set_kernel_timing(pt_renderer* r, int32_t enable) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_kernel_timing: NULL");
+    int rc = collect_pending(r);
+    if (rc) return rc;
+    r->kernel_timing = enable != 0;
     return PT_OK;
 }

@@ -530,7 +530,7 @@ void wavefront_free(WFState& W) {
 }
 
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
-                                  uint32_t frame, int cus, hipStream_t stream) {
+                                  uint32_t frame, int cus, hipStream_t stream, const hipEvent_t* trace_events) {
     const int P = L.width * L.height;
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
@@ -539,12 +539,14 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const bool fused = fused_mode(mode);
     for (int b = 0; b < maxb; ++b) {
+        if (trace_events && (e = hipEventRecord(trace_events[2 * b], stream)) != hipSuccess) return e;
         if (stats)
             hipLaunchKernelGGL(k_extend<true>, occupancy_grid(k_extend<true>, cus), dim3(kBlockWF), 0, stream, S, W,
                                b, L.counters);
         else
             hipLaunchKernelGGL(k_extend<false>, occupancy_grid(k_extend<false>, cus), dim3(kBlockWF), 0, stream, S,
                                W, b, L.counters);
+        if (trace_events && (e = hipEventRecord(trace_events[2 * b + 1], stream)) != hipSuccess) return e;
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (fused) {
             if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;

@@ -137,6 +137,10 @@ class OptixRenderer:
     def set_traversal_stats(self, enable: bool) -> None:
         check(self.lib.pt_set_traversal_stats(self.h, 1 if enable else 0), "pt_set_traversal_stats")
 
+    def set_kernel_timing(self, enable: bool = True) -> None:
+        """Time every wavefront closest-hit trace launch with its own HIP event pair."""
+        check(self.lib.pt_set_kernel_timing(self.h, 1 if enable else 0), "pt_set_kernel_timing")
+
     def accum_clear(self) -> None:
         check(self.lib.pt_accum_clear(self.h), "pt_accum_clear")
 
