@@ -13,10 +13,13 @@ accumulators are summed to rank 0 with one RCCL reduce (torch.distributed "nccl"
 over xGMI).  Per-GPU work is fixed as N grows ("weak" scaling); value = all samples of
 all ranks / max-over-ranks wall time.
 
-Extra fields: `roofline` (HBM roofline of the render kernel: algorithmic bytes per launch,
-SURVEY.md §8(d) 396 B/segment + 12 B/sample, over the per-launch average measured with
-HIP events on the library stream) and `cpu_baseline` (the CPU oracle, oracle/, timed on a
-bounded band of the same workload on the host cores, rank 0 at N=1 only).
+Extra fields: `roofline` (HBM roofline of the dominant kernel, the wavefront's closest-hit
+trace k_extend: 48 algorithmic bytes per traced segment, ray read + hit write, over its
+per-launch average measured with one HIP event pair per launch on the library stream;
+`pipeline_gbps` is SURVEY.md §8(d)'s whole-path 396 B/segment + 12 B/sample over the render
+time; `traffic` is the PMC HBM bytes per launch from profiles/traffic.json) and
+`cpu_baseline` (the CPU oracle, oracle/, timed on a bounded band of the same workload on the
+host cores, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
