@@ -69,10 +69,20 @@ struct TravStats {
 
 // Reciprocal direction; zero components map to a huge finite value so the fma slab form
 // never produces 0*inf.
+#ifndef PT_FAST_RCP
+#define PT_FAST_RCP 1
+#endif
+__device__ __forceinline__ float slab_rcp(float x) {
+#if PT_FAST_RCP
+    return __builtin_amdgcn_rcpf(x);  // 1 ulp; covered by the box padding and tfar widening
+#else
+    return 1.0f / x;
+#endif
+}
 __device__ __forceinline__ f3 safe_inv(f3 d) {
     const float big = 1e30f;
-    return mk(d.x != 0.0f ? 1.0f / d.x : copysignf(big, d.x), d.y != 0.0f ? 1.0f / d.y : copysignf(big, d.y),
-              d.z != 0.0f ? 1.0f / d.z : copysignf(big, d.z));
+    return mk(d.x != 0.0f ? slab_rcp(d.x) : copysignf(big, d.x), d.y != 0.0f ? slab_rcp(d.y) : copysignf(big, d.y),
+              d.z != 0.0f ? slab_rcp(d.z) : copysignf(big, d.z));
 }
 
 // Slab test of one child (lane c of the SoA node); boxes are padded at build time so the

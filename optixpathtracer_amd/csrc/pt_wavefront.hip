@@ -108,6 +108,11 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
 
 // This wave's static slice of a queue of length n (grid sized to residency, so every wave
 // is resident and slices balance statistically; no fetch atomics).
+#ifndef PT_REFILL_MIN
+#define PT_REFILL_MIN 8
+#endif
+constexpr int kRefillMin = PT_REFILL_MIN;
+
 __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
@@ -128,9 +133,11 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
     int ri = -1;
     while (true) {
         const bool need = ri < 0;
-        const unsigned long long m = __ballot(need ? 1 : 0);
+        unsigned long long m = __ballot(need ? 1 : 0);
+        // refill once enough lanes idle (the refill block costs the wave as much as a step)
+        if (__popcll(m) < kRefillMin && m != ~0ull && next < end) m = 0;
         const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (need && next + pre < end) {
+        if (need && m && next + pre < end) {
             ri = next + pre;
             fetch(ri, st);
             if (STATS) ts.rays++;
