@@ -35,6 +35,9 @@ extern "C" {
 /* Render-kernel variants (all produce the same image). */
 #define PT_KERNEL_MEGA 0      /* one thread per pixel, frames looped in registers */
 #define PT_KERNEL_WAVEFRONT 1 /* wavefront: per-bounce kernels over SoA ray/hit queues, wave compaction */
+#define PT_BVH_PLOC 0          /* GPU PLOC clustering -> BVH4 (default; near-SAH quality) */
+#define PT_BVH_LBVH 1          /* GPU Karras LBVH -> BVH4 (fastest build) */
+
 #define PT_KERNEL_AUTO 2      /* the faster path (measured): currently the wavefront in every mode */
 
 /* Mesh: ModelLoading/Mesh.h:9-45 (vertecies, normal, texCoord, index, ModelMatrix, albedo,
@@ -80,7 +83,8 @@ typedef struct pt_options {
     int32_t device;         /* HIP device ordinal (reference hard-codes device 0, OptixRenderer.cpp:70) */
     int32_t material_mode;  /* PT_MAT_* */
     int32_t kernel;         /* PT_KERNEL_* */
-    int32_t reserved[5];
+    int32_t bvh_builder;    /* PT_BVH_* (replaces optixAccelBuild, OptixRenderer.cpp:306-456) */
+    int32_t reserved[4];
 } pt_options;
 
 typedef struct pt_stats {

@@ -15,6 +15,7 @@ LIB_PATH = _HERE / "libptamd.so"
 
 PT_MAT_DEFAULT, PT_MAT_LAMBERT, PT_MAT_CONDUCTOR, PT_MAT_DIELECTRIC, PT_MAT_LAYERED = range(5)
 PT_KERNEL_MEGA, PT_KERNEL_WAVEFRONT, PT_KERNEL_AUTO = 0, 1, 2
+PT_BVH_PLOC, PT_BVH_LBVH = 0, 1
 
 MATERIAL_MODES = {
     "default": PT_MAT_DEFAULT,
@@ -69,7 +70,8 @@ class pt_options(C.Structure):
         ("device", C.c_int32),
         ("material_mode", C.c_int32),
         ("kernel", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("bvh_builder", C.c_int32),
+        ("reserved", C.c_int32 * 4),
     ]
 
 

@@ -11,6 +11,13 @@
 //   6. k_collapse : top-down, one launch per BVH4 level: each BVH4 node greedily opens its
 //                   largest-area binary child until it has 4 children; a binary subtree of
 //                   <= kLeafMax triangles (a contiguous leaf range) becomes a BVH4 leaf.
+// PLOC builder (Meister & Bittner 2018, "Parallel Locally-Ordered Clustering for Bounding
+// Volume Hierarchy Construction"), the default: starting from the Morton-sorted leaves, each
+// iteration finds every cluster's nearest neighbour (smallest merged surface area) within
+// +-kPlocRadius positions, merges mutual pairs and compacts (hipCUB scan).  A top-down pass
+// then numbers the leaves in depth-first order, so every subtree is again a contiguous
+// leaf range, and the same k_collapse turns it into BVH4.  Its SAH quality is close to a
+// full sweep build, which cuts traversal steps against the Karras tree.
 // Every kernel reads only what earlier launches wrote (no intra-launch hand-offs), so the
 // build needs no agent-scope fences; node numbering depends on atomic order but the
 // traversal result does not (closest hit is ordered by (t, triangle index)).  The sparse
@@ -242,7 +249,222 @@ __global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, 
     out[item.y] = nd;
 }
 
+
+// ---- PLOC ---------------------------------------------------------------------------------
+constexpr int kPlocRadius = 16;
+
+__device__ __forceinline__ float merged_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
+    float x = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);
+    float y = fmaxf(ahi.y, bhi.y) - fminf(alo.y, blo.y);
+    float z = fmaxf(ahi.z, bhi.z) - fminf(alo.z, blo.z);
+    return x * y + y * z + z * x;
+}
+
+// Leaf boxes in Morton order.
+__global__ void k_leafbox(const float4* tri_orig, const uint32_t* order, int n, float4* box, int* code, int* cnt) {
+    int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n) return;
+    float lo[3], hi[3];
+    tri_box(tri_orig, (int)order[m], lo, hi);
+    box[2 * m] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+    box[2 * m + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+    code[m] = ~m;
+    cnt[m] = 1;
+}
+
+// Nearest neighbour of every cluster within the window.  Ties go to the lower position,
+// which makes the globally best pair mutual (progress every iteration).
+__global__ void k_ploc_nn(const float4* box, int n, int* nn) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 lo = box[2 * i], hi = box[2 * i + 1];
+    unsigned long long best = ~0ull;
+    const int a = max(0, i - kPlocRadius), b = min(n - 1, i + kPlocRadius);
+    for (int j = a; j <= b; ++j) {
+        if (j == i) continue;
+        float c = merged_area(lo, hi, box[2 * j], box[2 * j + 1]);
+        unsigned long long key = ((unsigned long long)__float_as_uint(c) << 32) | (unsigned)j;
+        best = key < best ? key : best;
+    }
+    nn[i] = (int)(best & 0xffffffffu);
+}
+
+// flags: low 32 bits = cluster survives, high 32 bits = cluster creates a node.
+__global__ void k_ploc_flags(const int* nn, int n, unsigned long long* flags) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int j = nn[i];
+    const bool mutual = n > 1 && nn[j] == i;
+    const bool keep = !(mutual && i > j);
+    const bool merge = mutual && i < j;
+    flags[i] = ((unsigned long long)(merge ? 1 : 0) << 32) | (keep ? 1ull : 0ull);
+}
+
+__global__ void k_ploc_compact(const float4* box, const int* code, const int* cnt, const int* nn,
+                               const unsigned long long* scan, const unsigned long long* flags, int n,
+                               int node_base, float4* obox, int* ocode, int* ocnt, int2* bchild, float4* bbox,
+                               int* bcount) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long f = flags[i];
+    if (!(f & 1ull)) return;
+    const unsigned long long sc = scan[i];
+    const int pos = (int)(sc & 0xffffffffu);
+    float4 lo = box[2 * i], hi = box[2 * i + 1];
+    int c = code[i], k = cnt[i];
+    if (f >> 32) {
+        const int j = nn[i];
+        const float4 lj = box[2 * j], hj = box[2 * j + 1];
+        lo = make_float4(fminf(lo.x, lj.x), fminf(lo.y, lj.y), fminf(lo.z, lj.z), 0.0f);
+        hi = make_float4(fmaxf(hi.x, hj.x), fmaxf(hi.y, hj.y), fmaxf(hi.z, hj.z), 0.0f);
+        const int node = node_base + (int)(sc >> 32);
+        bchild[node] = make_int2(c, code[j]);
+        bbox[2 * node] = lo;
+        bbox[2 * node + 1] = hi;
+        bcount[node] = k + cnt[j];
+        c = node;
+        k += cnt[j];
+    }
+    obox[2 * pos] = lo;
+    obox[2 * pos + 1] = hi;
+    ocode[pos] = c;
+    ocnt[pos] = k;
+}
+
+// Depth-first leaf numbering, one launch per tree level: item = (node, first leaf).  Writes
+// the node's leaf range, rewrites leaf child codes from Morton positions to DFS positions
+// and records the triangle order.
+__global__ void k_ploc_dfs(const int2* work, int nwork, int2* bchild, const int* bcount, int2* brange,
+                           const uint32_t* morton_order, uint32_t* dfs_order, int2* next, int* nnext) {
+    int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwork) return;
+    const int2 it = work[w];
+    const int node = it.x, first = it.y;
+    brange[node] = make_int2(first, first + bcount[node] - 1);
+    int2 ch = bchild[node];
+    int c[2] = {ch.x, ch.y};
+    int f = first;
+    for (int k = 0; k < 2; ++k) {
+        if (c[k] < 0) {
+            dfs_order[f] = morton_order[~c[k]];
+            c[k] = ~f;
+            f += 1;
+        } else {
+            int q = atomicAdd(nnext, 1);
+            next[q] = make_int2(c[k], f);
+            f += bcount[c[k]];
+        }
+    }
+    bchild[node] = make_int2(c[0], c[1]);
+}
+
 inline unsigned grid_for(int n, int b) { return (unsigned)((n + b - 1) / b); }
+
+__global__ void k_ploc_total(const unsigned long long* scan, const unsigned long long* flags, int n, int* out) {
+    const unsigned long long t = scan[n - 1] + flags[n - 1];
+    out[0] = (int)(t & 0xffffffffu);  // surviving clusters
+    out[1] = (int)(t >> 32);          // nodes created
+}
+
+// Host sequencing of the PLOC iterations and the DFS numbering; fills B, the triangle
+// records in DFS leaf order and the binary root code.  One host sync per iteration / level
+// (the loop bounds come from device counts); allocations are appended to `owned`.
+hipError_t ploc_build(const BuildInput& in, const uint32_t* morton_order, BuildOutput& out, hipStream_t stream,
+                      BinTree& B, int& root, std::vector<void*>& owned) {
+    const int n = in.n;
+    hipError_t err = hipSuccess;
+    auto alloc = [&](void** p, size_t bytes) {
+        if (err == hipSuccess) err = hipMalloc(p, bytes > 0 ? bytes : 16);
+        if (err == hipSuccess) owned.push_back(*p);
+    };
+    const int nb = n > 1 ? n - 1 : 1;
+    float4 *box[2] = {nullptr, nullptr}, *bbox = nullptr, *leafbox = nullptr;
+    int *code[2] = {nullptr, nullptr}, *ccnt[2] = {nullptr, nullptr}, *nn = nullptr, *bcount = nullptr,
+        *tot = nullptr;
+    unsigned long long *flags = nullptr, *scan = nullptr;
+    int2 *bchild = nullptr, *brange = nullptr, *work[2] = {nullptr, nullptr};
+    uint32_t* dfs = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    for (int k = 0; k < 2; ++k) {
+        alloc((void**)&box[k], sizeof(float4) * 2 * (size_t)n);
+        alloc((void**)&code[k], sizeof(int) * (size_t)n);
+        alloc((void**)&ccnt[k], sizeof(int) * (size_t)n);
+        alloc((void**)&work[k], sizeof(int2) * (size_t)n);
+    }
+    alloc((void**)&nn, sizeof(int) * (size_t)n);
+    alloc((void**)&flags, sizeof(unsigned long long) * (size_t)n);
+    alloc((void**)&scan, sizeof(unsigned long long) * (size_t)n);
+    alloc((void**)&bchild, sizeof(int2) * (size_t)nb);
+    alloc((void**)&brange, sizeof(int2) * (size_t)nb);
+    alloc((void**)&bbox, sizeof(float4) * 2 * (size_t)nb);
+    alloc((void**)&bcount, sizeof(int) * (size_t)nb);
+    alloc((void**)&leafbox, sizeof(float4) * 2 * (size_t)n);
+    alloc((void**)&dfs, sizeof(uint32_t) * (size_t)n);
+    alloc((void**)&tot, sizeof(int) * 2);
+    if (err != hipSuccess) return err;
+    if ((err = hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, flags, scan, n, stream)) != hipSuccess)
+        return err;
+    alloc(&temp, temp_bytes);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(k_leafbox, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, morton_order, n, box[0],
+                       code[0], ccnt[0]);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    int cur = 0, m = n, node_base = 0;
+    while (m > 1) {
+        hipLaunchKernelGGL(k_ploc_nn, dim3(grid_for(m, 256)), dim3(256), 0, stream, box[cur], m, nn);
+        hipLaunchKernelGGL(k_ploc_flags, dim3(grid_for(m, 256)), dim3(256), 0, stream, nn, m, flags);
+        if ((err = hipGetLastError()) != hipSuccess) return err;
+        if ((err = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, flags, scan, m, stream)) != hipSuccess)
+            return err;
+        hipLaunchKernelGGL(k_ploc_compact, dim3(grid_for(m, 256)), dim3(256), 0, stream, box[cur], code[cur],
+                           ccnt[cur], nn, scan, flags, m, node_base, box[cur ^ 1], code[cur ^ 1], ccnt[cur ^ 1],
+                           bchild, bbox, bcount);
+        hipLaunchKernelGGL(k_ploc_total, dim3(1), dim3(1), 0, stream, scan, flags, m, tot);
+        if ((err = hipGetLastError()) != hipSuccess) return err;
+        int h[2] = {0, 0};
+        if ((err = hipMemcpyAsync(h, tot, sizeof h, hipMemcpyDeviceToHost, stream)) != hipSuccess) return err;
+        if ((err = hipStreamSynchronize(stream)) != hipSuccess) return err;
+        if (h[1] <= 0) return hipErrorUnknown;  // cannot happen: the best pair is always mutual
+        m = h[0];
+        node_base += h[1];
+        cur ^= 1;
+    }
+    int rc = ~0;
+    if ((err = hipMemcpyAsync(&rc, code[cur], sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess) return err;
+    if ((err = hipStreamSynchronize(stream)) != hipSuccess) return err;
+    root = rc;
+    if (rc < 0) {  // single triangle
+        if ((err = hipMemcpyAsync(dfs, morton_order, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream)) !=
+            hipSuccess)
+            return err;
+        root = ~0;
+    } else {
+        int2 w0 = make_int2(rc, 0);
+        int nwork = 1, c = 0;
+        int* nnext = tot;
+        if ((err = hipMemcpyAsync(work[0], &w0, sizeof(int2), hipMemcpyHostToDevice, stream)) != hipSuccess)
+            return err;
+        while (nwork > 0) {
+            if ((err = hipMemsetAsync(nnext, 0, sizeof(int), stream)) != hipSuccess) return err;
+            hipLaunchKernelGGL(k_ploc_dfs, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, work[c], nwork, bchild,
+                               bcount, brange, morton_order, dfs, work[c ^ 1], nnext);
+            if ((err = hipGetLastError()) != hipSuccess) return err;
+            if ((err = hipMemcpyAsync(&nwork, nnext, sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess)
+                return err;
+            if ((err = hipStreamSynchronize(stream)) != hipSuccess) return err;
+            c ^= 1;
+        }
+    }
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig, dfs, n,
+                       out.isect, out.shade, leafbox);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    B.child = bchild;
+    B.range = brange;
+    B.box = bbox;
+    B.leafbox = leafbox;
+    return hipSuccess;
+}
 
 }  // namespace
 
@@ -269,8 +491,10 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     SparseTable table{};
     BinTree B{};
     int h_cnt[2] = {1, 0};
-    int nwork = 1, depth = 0;
+    int nwork = 1, depth = 0, root = 0;
     const int nbin = n > 1 ? n - 1 : 1;
+    const bool ploc = in.builder != kBuilderLBVH;
+    std::vector<void*> owned;
     if (ms) *ms = 0.0f;
     out.n_nodes = 0;
     out.depth = 0;
@@ -282,10 +506,12 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     PT_TRY(hipMalloc(&vals, sizeof(uint32_t) * n));
     PT_TRY(hipMalloc(&keys2, sizeof(uint32_t) * n));
     PT_TRY(hipMalloc(&vals2, sizeof(uint32_t) * n));
-    PT_TRY(hipMalloc(&st, sizeof(float4) * 2 * (size_t)n * (size_t)levels));
-    PT_TRY(hipMalloc(&bchild, sizeof(int2) * nbin));
-    PT_TRY(hipMalloc(&brange, sizeof(int2) * nbin));
-    PT_TRY(hipMalloc(&bbox, sizeof(float4) * 2 * nbin));
+    if (!ploc) {
+        PT_TRY(hipMalloc(&st, sizeof(float4) * 2 * (size_t)n * (size_t)levels));
+        PT_TRY(hipMalloc(&bchild, sizeof(int2) * nbin));
+        PT_TRY(hipMalloc(&brange, sizeof(int2) * nbin));
+        PT_TRY(hipMalloc(&bbox, sizeof(float4) * 2 * nbin));
+    }
     PT_TRY(hipMalloc(&work, sizeof(int2) * n));
     PT_TRY(hipMalloc(&work2, sizeof(int2) * n));
     PT_TRY(hipMalloc(&cnt, sizeof(int) * 2));
@@ -301,32 +527,37 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
                            vals);
         PT_TRY(hipGetLastError());
         PT_TRY(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, n, 0, 30, stream));
-        hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig, vals2,
-                           n, out.isect, out.shade, st);
-        PT_TRY(hipGetLastError());
-        table.n = n;
-        table.level[0] = st;
-        for (int l = 1; l < levels; ++l) {
-            float4* prev = st + 2 * (size_t)n * (size_t)(l - 1);
-            float4* cur = st + 2 * (size_t)n * (size_t)l;
-            int count = n - (1 << l) + 1;
-            hipLaunchKernelGGL(k_sparse, dim3(grid_for(count, 256)), dim3(256), 0, stream, prev, cur, count,
-                               1 << (l - 1));
+        if (ploc) {
+            PT_TRY(ploc_build(in, vals2, out, stream, B, root, owned));
+        } else {
+            hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig,
+                               vals2, n, out.isect, out.shade, st);
             PT_TRY(hipGetLastError());
-            table.level[l] = cur;
+            table.n = n;
+            table.level[0] = st;
+            for (int l = 1; l < levels; ++l) {
+                float4* prev = st + 2 * (size_t)n * (size_t)(l - 1);
+                float4* cur = st + 2 * (size_t)n * (size_t)l;
+                int count = n - (1 << l) + 1;
+                hipLaunchKernelGGL(k_sparse, dim3(grid_for(count, 256)), dim3(256), 0, stream, prev, cur, count,
+                                   1 << (l - 1));
+                PT_TRY(hipGetLastError());
+                table.level[l] = cur;
+            }
+            if (n > 1) {
+                hipLaunchKernelGGL(k_karras, dim3(grid_for(n - 1, 256)), dim3(256), 0, stream, keys2, n, table,
+                                   bchild, brange, bbox);
+                PT_TRY(hipGetLastError());
+            }
+            B.child = bchild;
+            B.range = brange;
+            B.box = bbox;
+            B.leafbox = st;
+            root = n > 1 ? 0 : ~0;
         }
-        if (n > 1) {
-            hipLaunchKernelGGL(k_karras, dim3(grid_for(n - 1, 256)), dim3(256), 0, stream, keys2, n, table, bchild,
-                               brange, bbox);
-            PT_TRY(hipGetLastError());
-        }
-        B.child = bchild;
-        B.range = brange;
-        B.box = bbox;
-        B.leafbox = st;
-        // root work item: binary node 0 (or the single leaf ~0) -> BVH4 slot 0
-        int2 root = make_int2(n > 1 ? 0 : ~0, 0);
-        PT_TRY(hipMemcpyAsync(work, &root, sizeof(int2), hipMemcpyHostToDevice, stream));
+        // root work item: binary root (or the single leaf ~0) -> BVH4 slot 0
+        int2 rw = make_int2(root, 0);
+        PT_TRY(hipMemcpyAsync(work, &rw, sizeof(int2), hipMemcpyHostToDevice, stream));
         PT_TRY(hipMemcpyAsync(cnt, h_cnt, sizeof(int) * 2, hipMemcpyHostToDevice, stream));
         while (nwork > 0) {
             PT_TRY(hipMemsetAsync(cnt + 1, 0, sizeof(int), stream));
@@ -348,9 +579,11 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     out.n_nodes = h_cnt[0];
     out.depth = depth;
 done:
+    (void)hipStreamSynchronize(stream);
     for (void* p : {(void*)keys, (void*)vals, (void*)keys2, (void*)vals2, (void*)st, (void*)bchild, (void*)brange,
                     (void*)bbox, (void*)work, (void*)work2, (void*)cnt, temp})
         if (p) (void)hipFree(p);
+    for (void* p : owned) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     return err;

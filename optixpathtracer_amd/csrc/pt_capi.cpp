@@ -254,6 +254,8 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     pt_options opt{};
     if (options) opt = *options;
     if (!valid_mode(opt.material_mode)) return fail(PT_ERR_INVALID, "pt_create: invalid material_mode");
+    if (opt.bvh_builder != PT_BVH_PLOC && opt.bvh_builder != PT_BVH_LBVH)
+        return fail(PT_ERR_INVALID, "pt_create: invalid bvh_builder");
     if (opt.kernel != PT_KERNEL_MEGA && opt.kernel != PT_KERNEL_WAVEFRONT && opt.kernel != PT_KERNEL_AUTO)
         return fail(PT_ERR_INVALID, "pt_create: invalid kernel");
     int ndev = 0;
@@ -355,6 +357,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         in.tri_orig = d_tri_orig;
         in.nrm_orig = d_nrm_orig;
         in.n = (int)ntri;
+        in.builder = opt.bvh_builder == PT_BVH_LBVH ? kBuilderLBVH : kBuilderPLOC;
         for (int a = 0; a < 3; ++a) {
             in.cmin[a] = cmin[a];
             in.cmax[a] = cmax[a];

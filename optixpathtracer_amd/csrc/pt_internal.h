@@ -15,7 +15,10 @@ struct BuildInput {
     const float4* nrm_orig;  // 3 per triangle
     int n;
     float cmin[3], cmax[3];  // centroid bounds (Morton quantisation range)
+    int builder;             // kBuilderPLOC (default) or kBuilderLBVH
 };
+constexpr int kBuilderPLOC = 0;
+constexpr int kBuilderLBVH = 1;
 
 // BVH4 (collapsed LBVH) + triangle records in leaf order.
 struct BuildOutput {

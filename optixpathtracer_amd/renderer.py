@@ -74,7 +74,7 @@ class OptixRenderer:
     """Drop-in for `OptixRenderer` (OptixRenderer.h:8-110) backed by libptamd.so."""
 
     def __init__(self, ptx_path_or_none, model: Scene, device: int = 0, material_mode: int | None = None,
-                 kernel: int = capi.PT_KERNEL_AUTO):
+                 kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC):
         # ptxPath is accepted for signature compatibility and ignored (no PTX on gfx950).
         self.lib = load()
         self.model = model
@@ -83,6 +83,7 @@ class OptixRenderer:
         opts.device = int(device)
         opts.material_mode = int(model.material_mode if material_mode is None else material_mode)
         opts.kernel = int(kernel)
+        opts.bvh_builder = int(bvh_builder)
         h = C.c_void_p()
         check(self.lib.pt_create(C.byref(self._binding.scene), C.byref(opts), C.byref(h)), "pt_create")
         self.h = h
@@ -204,9 +205,9 @@ class OptixRenderer:
 
 
 def setup_renderer(scene: Scene, width: int, height: int, max_bounces: int, device: int = 0,
-                   kernel: int = capi.PT_KERNEL_AUTO) -> OptixRenderer:
+                   kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC) -> OptixRenderer:
     """The reference's main.cpp:95-113 sequence: construct, Resize, SetLights, SetMaxBounces, SetCamera."""
-    r = OptixRenderer(None, scene, device=device, kernel=kernel)
+    r = OptixRenderer(None, scene, device=device, kernel=kernel, bvh_builder=bvh_builder)
     r.Resize((width, height))
     r.SetLights(scene.lights)
     r.SetMaxBounces(max_bounces)

@@ -31,12 +31,13 @@ def diffuse_scene():
     return scenes.sphere_in_box("diffuse")
 
 
-def test_trace_closest_bit_exact(diffuse_scene):
+@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+def test_trace_closest_bit_exact(diffuse_scene, builder):
     from optixpathtracer_amd.renderer import setup_renderer
     from oracle.oracle import OracleScene
 
     rays = random_rays(diffuse_scene, 3000, seed=1)
-    r = setup_renderer(diffuse_scene, 64, 64, 4)
+    r = setup_renderer(diffuse_scene, 64, 64, 4, bvh_builder=builder)
     gp, gt, gu, gv, gb = r.trace_rays(rays)
     o = OracleScene(diffuse_scene)
     op, ot, ou, ov, ob = o.trace(rays)
@@ -54,7 +55,54 @@ def test_trace_closest_bit_exact(diffuse_scene):
     r.close()
 
 
-def test_trace_empty_and_single_triangle():
+@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+def test_trace_sponza_class_bit_exact(builder):
+    """~250k triangles: deeper trees, many PLOC iterations, LDS-stack spills."""
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import setup_renderer
+    from oracle.oracle import OracleScene
+
+    sc = scenes.sponza_class()
+    rays = random_rays(sc, 2000, seed=7)
+    r = setup_renderer(sc, 32, 32, 2, bvh_builder=builder)
+    gp, gt, gu, gv, gb = r.trace_rays(rays)
+    st = r.stats()
+    o = OracleScene(sc)
+    op, ot, ou, ov, ob = o.trace(rays)
+    assert (gp >= 0).sum() > 500
+    np.testing.assert_array_equal(gp, op)
+    hit = op >= 0
+    np.testing.assert_array_equal(gt[hit], ot[hit])
+    np.testing.assert_array_equal(gu[hit], ou[hit])
+    np.testing.assert_array_equal(gv[hit], ov[hit])
+    ga = r.trace_rays(rays, any_hit=True)[0] >= 0
+    oa = o.trace(rays, any_hit=True)[0] >= 0
+    np.testing.assert_array_equal(ga, oa)
+    assert st["bvh_nodes"] > 0 and st["triangles"] == sc.n_triangles
+    r.close()
+    o.close()
+
+
+@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+def test_trace_two_triangles(builder):
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import OptixRenderer
+
+    two = scenes.Mesh(vertices=np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]], np.float32),
+                      indices=np.array([[0, 1, 2], [0, 2, 3]], np.int32),
+                      normals=np.array([[0, 0, 1]] * 4, np.float32))
+    sc = scenes.Scene(meshes=[two], lights=np.zeros((0, 6), np.float32), camera_blender_pos=(0, 0, 0),
+                      camera_blender_rot=(0, 0, 0))
+    r = OptixRenderer(None, sc, bvh_builder=builder)
+    rays = np.array([[0.75, 0.25, 1, 0, 0, -1, 0, 10], [0.25, 0.75, 1, 0, 0, -1, 0, 10],
+                     [2, 2, 1, 0, 0, -1, 0, 10]], dtype=np.float32)
+    p = r.trace_rays(rays)[0]
+    assert list(p) == [0, 1, -1]
+    r.close()
+
+
+@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+def test_trace_empty_and_single_triangle(builder):
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import OptixRenderer
 
@@ -63,7 +111,7 @@ def test_trace_empty_and_single_triangle():
                       normals=np.array([[0, 0, 1]] * 3, np.float32))
     sc = scenes.Scene(meshes=[one], lights=np.zeros((0, 6), np.float32), camera_blender_pos=(0, 0, 0),
                       camera_blender_rot=(0, 0, 0))
-    r = OptixRenderer(None, sc)
+    r = OptixRenderer(None, sc, bvh_builder=builder)
     rays = np.array([[0.2, 0.2, 1, 0, 0, -1, 0, 100], [2, 2, 1, 0, 0, -1, 0, 100],
                      [0.2, 0.2, -1, 0, 0, 1, 0, 100]], np.float32)
     p, t, u, v, b = r.trace_rays(rays)
@@ -73,7 +121,7 @@ def test_trace_empty_and_single_triangle():
     r.close()
     empty = scenes.Scene(meshes=[], lights=np.zeros((0, 6), np.float32), camera_blender_pos=(0, 0, 0),
                          camera_blender_rot=(0, 0, 0))
-    r = OptixRenderer(None, empty)
+    r = OptixRenderer(None, empty, bvh_builder=builder)
     assert list(r.trace_rays(rays)[0]) == [-1, -1, -1]
     r.Resize((8, 8))
     r.SetCameraBlender((0, 0, 0), (90, 0, 0))

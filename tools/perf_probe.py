@@ -27,51 +27,54 @@ def main():
     ap.add_argument("--fpl", default="8")
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--builders", default="0", help="0 = PLOC, 1 = LBVH")
     a = ap.parse_args()
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import setup_renderer
 
     sc = scenes.make_scene(a.scene)
     modes = [int(m) for m in a.modes.split(",")] if a.modes else [sc.material_mode]
-    t0 = time.time()
-    r = setup_renderer(sc, a.width, a.height, a.depth)
-    st = r.stats()
-    print(json.dumps({"scene": a.scene, "tris": sc.n_triangles, "setup_s": round(time.time() - t0, 2),
-                      "bvh_ms": round(st["bvh_build_ms"], 3), "bvh_nodes": st["bvh_nodes"],
-                      "bvh_depth": st["bvh_depth"]}), flush=True)
-    for kernel in [int(k) for k in a.kernels.split(",")]:
-        for mode in modes:
-            for fpl in [int(f) for f in a.fpl.split(",")]:
-                r.set_kernel(kernel)
-                r.set_material_mode(mode)
-                r.set_frames_per_launch(fpl)
-                r.accum_clear()
-                r.render_frames(1, min(a.spp, 2))  # warm
-                r.synchronize()
-                best = None
-                for rep in range(a.repeat):
-                    r.stats_reset()
-                    r.render_frames(1 + 1000 * rep, a.spp)
-                    s = r.stats()
-                    ms = s["total_render_ms"]
-                    best = ms if best is None else min(best, ms)
-                samples = a.width * a.height * a.spp
-                out = {"kernel": kernel, "mode": mode, "fpl": fpl, "kernel_ms": round(best, 2),
-                       "msamples_s": round(samples / best / 1e3, 2),
-                       "segments_per_sample": round(s["segments"] / samples, 4)}
-                if a.stats:
-                    r.set_traversal_stats(True)
-                    r.stats_reset()
-                    r.render_frames(1, max(1, a.spp // 4))
-                    s = r.stats()
-                    r.set_traversal_stats(False)
-                    rays = max(1, s["rays"])
-                    out.update({"nodes_per_ray": round(s["nodes_visited"] / rays, 2),
-                                "tris_per_ray": round(s["tri_tests"] / rays, 2),
-                                "rays_per_sample": round(rays / (a.width * a.height * max(1, a.spp // 4)), 3),
-                                "stack_overflows": s["stack_overflows"]})
-                print(json.dumps(out), flush=True)
-    r.close()
+    for builder in [int(b) for b in a.builders.split(",")]:
+        t0 = time.time()
+        r = setup_renderer(sc, a.width, a.height, a.depth, bvh_builder=builder)
+        st = r.stats()
+        print(json.dumps({"scene": a.scene, "tris": sc.n_triangles, "builder": builder,
+                          "setup_s": round(time.time() - t0, 2),
+                          "bvh_ms": round(st["bvh_build_ms"], 3), "bvh_nodes": st["bvh_nodes"],
+                          "bvh_depth": st["bvh_depth"]}), flush=True)
+        for kernel in [int(k) for k in a.kernels.split(",")]:
+            for mode in modes:
+                for fpl in [int(f) for f in a.fpl.split(",")]:
+                    r.set_kernel(kernel)
+                    r.set_material_mode(mode)
+                    r.set_frames_per_launch(fpl)
+                    r.accum_clear()
+                    r.render_frames(1, min(a.spp, 2))  # warm
+                    r.synchronize()
+                    best = None
+                    for rep in range(a.repeat):
+                        r.stats_reset()
+                        r.render_frames(1 + 1000 * rep, a.spp)
+                        s = r.stats()
+                        ms = s["total_render_ms"]
+                        best = ms if best is None else min(best, ms)
+                    samples = a.width * a.height * a.spp
+                    out = {"kernel": kernel, "mode": mode, "fpl": fpl, "kernel_ms": round(best, 2),
+                           "msamples_s": round(samples / best / 1e3, 2),
+                           "segments_per_sample": round(s["segments"] / samples, 4)}
+                    if a.stats:
+                        r.set_traversal_stats(True)
+                        r.stats_reset()
+                        r.render_frames(1, max(1, a.spp // 4))
+                        s = r.stats()
+                        r.set_traversal_stats(False)
+                        rays = max(1, s["rays"])
+                        out.update({"nodes_per_ray": round(s["nodes_visited"] / rays, 2),
+                                    "tris_per_ray": round(s["tri_tests"] / rays, 2),
+                                    "rays_per_sample": round(rays / (a.width * a.height * max(1, a.spp // 4)), 3),
+                                    "stack_overflows": s["stack_overflows"]})
+                    print(json.dumps(out), flush=True)
+        r.close()
 
 
 if __name__ == "__main__":
