@@ -251,7 +251,10 @@ __global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, 
 
 
 // ---- PLOC ---------------------------------------------------------------------------------
-constexpr int kPlocRadius = 16;
+#ifndef PT_PLOC_RADIUS
+#define PT_PLOC_RADIUS 8
+#endif
+constexpr int kPlocRadius = PT_PLOC_RADIUS;
 
 __device__ __forceinline__ float merged_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
     float x = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);

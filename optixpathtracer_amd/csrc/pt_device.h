@@ -18,7 +18,10 @@
 
 namespace pt {
 
-constexpr int kLeafMax = 4;
+#ifndef PT_LEAF_MAX
+#define PT_LEAF_MAX 2
+#endif
+constexpr int kLeafMax = PT_LEAF_MAX;
 constexpr int kEmptyChild = (int)0x80000000;
 
 struct __align__(16) BNode4 {
@@ -69,6 +72,9 @@ struct TravStats {
 
 // Reciprocal direction; zero components map to a huge finite value so the fma slab form
 // never produces 0*inf.
+#ifndef PT_ANY_UNSORTED
+#define PT_ANY_UNSORTED 1
+#endif
 #ifndef PT_FAST_RCP
 #define PT_FAST_RCP 1
 #endif
@@ -215,16 +221,18 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         int c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
         int c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
         int c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
-        t0 = c0 != kEmptyChild ? t0 : inf;
-        t1 = c1 != kEmptyChild ? t1 : inf;
-        t2 = c2 != kEmptyChild ? t2 : inf;
-        t3 = c3 != kEmptyChild ? t3 : inf;
-        // sort ascending (optimal 4-network); misses sink to the end with t = inf
-        cswap(t0, c0, t1, c1);
-        cswap(t2, c2, t3, c3);
-        cswap(t0, c0, t2, c2);
-        cswap(t1, c1, t3, c3);
-        cswap(t1, c1, t2, c2);
+        if (!ANY || !PT_ANY_UNSORTED) {
+            t0 = c0 != kEmptyChild ? t0 : inf;
+            t1 = c1 != kEmptyChild ? t1 : inf;
+            t2 = c2 != kEmptyChild ? t2 : inf;
+            t3 = c3 != kEmptyChild ? t3 : inf;
+            // sort ascending (optimal 4-network); misses sink to the end with t = inf
+            cswap(t0, c0, t1, c1);
+            cswap(t2, c2, t3, c3);
+            cswap(t0, c0, t2, c2);
+            cswap(t1, c1, t3, c3);
+            cswap(t1, c1, t2, c2);
+        }  // any-hit: visit order does not change the answer, skip the sort
         // push the farther hits (far first), continue with the nearest
         if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
         {  // unconditional stores, predicated sp: an empty child's store lands in the slot
