@@ -179,6 +179,32 @@ int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* pr
 const char* pt_last_error(void);
 const char* pt_version(void);
 
+/* ---- headless progressive view --------------------------------
+ * OptixView::AddNewFrameToBuffer (Renderer/OptixView.cpp:226-255) + AddPathtracedFrame.frag
+ * :18-24 on the device.  pt_display_reset clears the view buffer to 1.0 (glClearColor(1,1,1,1),
+ * OptixView.cpp:145-149) and sets maxSamples; each pt_display_add_frame renders one spp like
+ * pt_render (frame.id++) and blends it: max_samples < 0 -> fb = mix(fb, new, 1/n) (running
+ * mean), else fb += new * (1/max_samples).  *samples (optional) receives n. */
+int pt_display_reset(pt_renderer* r, int32_t max_samples);
+int pt_display_add_frame(pt_renderer* r, int32_t* samples);
+int pt_display_download(pt_renderer* r, float* rgb);
+
+/* ---- image output and the parity metric ----------------------
+ * Renderer/Images/WriteImage.cpp:35-99 (WriteEXR): float32 B,G,R scanline EXR, uncompressed,
+ * rows flipped (rgb row 0 = bottom, as colorBuffer), a pixel with a NaN channel written as 0. */
+int pt_image_write_exr(const char* path, const float* rgb, int32_t width, int32_t height);
+/* WriteImage.cpp:8-32 (WriteBMP): clamp(v, 0, 1) * 255 truncated, 24-bit BMP. */
+int pt_image_write_bmp(const char* path, const float* rgb, int32_t width, int32_t height);
+/* Little-endian colour PFM, bottom row first. */
+int pt_image_write_pfm(const char* path, const float* rgb, int32_t width, int32_t height);
+/* Reads an uncompressed scanline EXR (half or float R,G,B) or a colour PFM into rgb (row 0 =
+ * bottom).  rgb = NULL only returns the size. */
+int pt_image_read(const char* path, float* rgb, int32_t* width, int32_t* height);
+/* Per-image parity metric of SURVEY.md §8(c): mean over pixels x 3 channels of (a - b)^2,
+ * pixels with a NaN channel counted as 0 (as the reference's EXR writer stores them). */
+double pt_image_mse(const float* a, const float* b, int64_t n_pixels);
+const char* pt_image_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

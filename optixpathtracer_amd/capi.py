@@ -130,6 +130,15 @@ SIGNATURES = {
     "pt_trace_rays": (C.c_int, [_R, _FP, C.c_int32, _IP, _FP, _FP, _FP, _IP, C.c_int32]),
     "pt_last_error": (C.c_char_p, []),
     "pt_version": (C.c_char_p, []),
+    "pt_display_reset": (C.c_int, [_R, C.c_int32]),
+    "pt_display_add_frame": (C.c_int, [_R, C.POINTER(C.c_int32)]),
+    "pt_display_download": (C.c_int, [_R, _FP]),
+    "pt_image_write_exr": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),
+    "pt_image_write_bmp": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),
+    "pt_image_write_pfm": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),
+    "pt_image_read": (C.c_int, [C.c_char_p, _FP, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "pt_image_mse": (C.c_double, [_FP, _FP, C.c_int64]),
+    "pt_image_last_error": (C.c_char_p, []),
 }
 
 _lib = None

@@ -109,6 +109,10 @@ struct pt_renderer {
     uint32_t frame_id = 0;
     // buffers
     float* d_frame = nullptr;   // 1-spp frame (pt_render)
+    float* d_display = nullptr;  // progressive view buffer (pt_display_*)
+    int display_max = -1;
+    int display_samples = 0;
+    bool display_ready = false;
     float* d_accum = nullptr;   // internal sum buffer
     float* user_accum = nullptr;
     unsigned long long* d_counters = nullptr;
@@ -393,6 +397,7 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_lights) (void)hipFree(r->d_lights);
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->d_accum) (void)hipFree(r->d_accum);
+    if (r->d_display) (void)hipFree(r->d_display);
     if (r->d_counters) (void)hipFree(r->d_counters);
     wavefront_free(r->wf);
     r->ev.destroy();
@@ -411,7 +416,9 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
     size_t bytes = sizeof(float) * 3 * (size_t)width * (size_t)height;
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->d_accum) (void)hipFree(r->d_accum);
-    r->d_frame = r->d_accum = nullptr;
+    if (r->d_display) (void)hipFree(r->d_display);
+    r->d_frame = r->d_accum = r->d_display = nullptr;
+    r->display_ready = false;
     PT_HIP(hipMalloc(&r->d_frame, bytes), "hipMalloc frame");
     PT_HIP(hipMalloc(&r->d_accum, bytes), "hipMalloc accum");
     PT_HIP(hipMemsetAsync(r->d_accum, 0, bytes, r->stream), "hipMemset accum");
@@ -485,6 +492,46 @@ int pt_render(pt_renderer* r, float* host_rgb) {
     int rc = launch_frames(r, r->d_frame, r->frame_id, 1);
     if (rc) return rc;
     PT_HIP(hipMemcpyAsync(host_rgb, r->d_frame, bytes, hipMemcpyDeviceToHost, r->stream), "download frame");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    return collect_pending(r);
+}
+
+int pt_display_reset(pt_renderer* r, int32_t max_samples) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_display_reset: NULL");
+    if (r->width == 0) return fail(PT_ERR_STATE, "pt_display_reset: call pt_resize first");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    const size_t n = 3 * (size_t)r->width * (size_t)r->height;
+    if (!r->d_display) PT_HIP(hipMalloc(&r->d_display, sizeof(float) * n), "hipMalloc display");
+    PT_HIP(display_fill(r->d_display, n, 1.0f, r->stream), "display clear");  // glClearColor(1,1,1,1)
+    r->display_max = max_samples;
+    r->display_samples = 0;
+    r->display_ready = true;
+    return PT_OK;
+}
+
+int pt_display_add_frame(pt_renderer* r, int32_t* samples) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_display_add_frame: NULL");
+    if (!r->display_ready) return fail(PT_ERR_STATE, "pt_display_add_frame: call pt_display_reset first");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    r->frame_id++;  // Render: OptixRenderer.cpp:623
+    const size_t n = 3 * (size_t)r->width * (size_t)r->height;
+    PT_HIP(hipMemsetAsync(r->d_frame, 0, sizeof(float) * n, r->stream), "hipMemset frame");
+    int rc = launch_frames(r, r->d_frame, r->frame_id, 1);
+    if (rc) return rc;
+    r->display_samples++;  // OptixView.cpp:239-248
+    const bool continuous = r->display_max < 0;
+    const float w = continuous ? 1.0f / (float)r->display_samples : 1.0f / (float)r->display_max;
+    PT_HIP(display_blend(r->d_display, r->d_frame, n, w, continuous, r->stream), "display blend");
+    if (samples) *samples = r->display_samples;
+    return PT_OK;
+}
+
+int pt_display_download(pt_renderer* r, float* host_rgb) {
+    if (!r || !host_rgb) return fail(PT_ERR_INVALID, "pt_display_download: NULL");
+    if (!r->display_ready) return fail(PT_ERR_STATE, "pt_display_download: call pt_display_reset first");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    const size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
+    PT_HIP(hipMemcpyAsync(host_rgb, r->d_display, bytes, hipMemcpyDeviceToHost, r->stream), "download display");
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     return collect_pending(r);
 }

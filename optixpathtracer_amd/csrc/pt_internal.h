@@ -64,4 +64,8 @@ hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, co
 hipError_t launch_trace(const DevScene& S, const float* d_rays, int n, int* d_prim, float* d_thit, float* d_u,
                         float* d_v, int* d_back, int any_hit, hipStream_t stream);
 
+// Progressive view buffer (pt_display.hip).
+hipError_t display_fill(float* p, size_t n, float v, hipStream_t stream);
+hipError_t display_blend(float* fb, const float* frame, size_t n, float w, bool continuous, hipStream_t stream);
+
 }  // namespace pt

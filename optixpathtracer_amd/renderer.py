@@ -142,6 +142,21 @@ class OptixRenderer:
         """Time every wavefront closest-hit trace launch with its own HIP event pair."""
         check(self.lib.pt_set_kernel_timing(self.h, 1 if enable else 0), "pt_set_kernel_timing")
 
+    # -- headless progressive view (OptixView accumulation on the device) -------------------
+    def display_reset(self, max_samples: int = -1) -> None:
+        check(self.lib.pt_display_reset(self.h, int(max_samples)), "pt_display_reset")
+
+    def display_add_frame(self) -> int:
+        n = C.c_int32(0)
+        check(self.lib.pt_display_add_frame(self.h, C.byref(n)), "pt_display_add_frame")
+        return n.value
+
+    def display(self) -> np.ndarray:
+        w, h = self.size
+        out = np.empty((h, w, 3), dtype=np.float32)
+        check(self.lib.pt_display_download(self.h, fptr(out)), "pt_display_download")
+        return out
+
     def accum_clear(self) -> None:
         check(self.lib.pt_accum_clear(self.h), "pt_accum_clear")
 
