@@ -74,10 +74,21 @@ class OptixRendererT {
             pm.metal_rough_tex = me.metalRoughTex;
             meshes.push_back(pm);
         }
+        // Model::textures (Texture.h:5-12: uint32_t* pixel RGBA8, ivec2 resolution)
+        std::vector<pt_texture> textures;
+        for (auto& tp : m->textures) {
+            pt_texture t;
+            t.rgba8 = tp->pixel;
+            t.width = (int32_t)tp->resolution.x;
+            t.height = (int32_t)tp->resolution.y;
+            textures.push_back(t);
+        }
         pt_scene sc;
         std::memset(&sc, 0, sizeof sc);
         sc.meshes = meshes.data();
         sc.n_meshes = (int32_t)meshes.size();
+        sc.textures = textures.empty() ? nullptr : textures.data();
+        sc.n_textures = (int32_t)textures.size();
         pt_options opt;
         std::memset(&opt, 0, sizeof opt);
         opt.device = device;

@@ -189,6 +189,25 @@ int pt_display_reset(pt_renderer* r, int32_t max_samples);
 int pt_display_add_frame(pt_renderer* r, int32_t* samples);
 int pt_display_download(pt_renderer* r, float* rgb);
 
+/* ---- glTF scene loading -----------------------------------------
+ * ModelLoader::LoadModel (ModelLoading/ModelLoader.cpp:10-244): glTF 2.0 (.gltf with external
+ * or data-URI buffers, or .glb) -> an owned pt_scene for pt_create.  One mesh per triangle
+ * primitive, node transforms T*R*S composed down the hierarchy, baseColor / metallic /
+ * roughness factors and texture ids, textures as RGBA8.  PNG is decoded internally; other
+ * image formats (JPEG, ...; stb_image in the reference) go through `decode`, which is called
+ * with rgba_out = NULL for the size and then with a width*height*4-byte buffer, and returns
+ * 0 on success.  Deviations from the reference loader's bugs are listed in pt_gltf.cpp. */
+typedef struct pt_model pt_model;
+typedef int (*pt_image_decode_fn)(const uint8_t* data, size_t size, int32_t* width, int32_t* height,
+                                  uint8_t* rgba_out, void* user);
+int pt_model_load_gltf(const char* path, pt_image_decode_fn decode, void* user, pt_model** out);
+const pt_scene* pt_model_scene(const pt_model* m);
+const char* pt_model_mesh_name(const pt_model* m, int32_t index);
+int pt_model_destroy(pt_model* m);
+const char* pt_model_last_error(void);
+/* The loader's PNG decoder (RGBA8, rows as stored); rgba_out = NULL returns the size. */
+int pt_image_decode_png(const uint8_t* data, size_t size, int32_t* width, int32_t* height, uint8_t* rgba_out);
+
 /* ---- image output and the parity metric ----------------------
  * Renderer/Images/WriteImage.cpp:35-99 (WriteEXR): float32 B,G,R scanline EXR, uncompressed,
  * rows flipped (rgb row 0 = bottom, as colorBuffer), a pixel with a NaN channel written as 0. */

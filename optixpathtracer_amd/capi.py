@@ -100,6 +100,10 @@ class pt_stats(C.Structure):
 _FP = C.POINTER(C.c_float)
 _IP = C.POINTER(C.c_int32)
 _R = C.c_void_p  # pt_renderer*
+_M = C.c_void_p  # pt_model*
+# int decode(const uint8_t* data, size_t size, int32_t* w, int32_t* h, uint8_t* rgba_out, void* user)
+pt_image_decode_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                 C.c_void_p, C.c_void_p)
 
 # name -> (restype, argtypes); this is the complete exported surface of include/ptamd.h
 SIGNATURES = {
@@ -133,6 +137,13 @@ SIGNATURES = {
     "pt_display_reset": (C.c_int, [_R, C.c_int32]),
     "pt_display_add_frame": (C.c_int, [_R, C.POINTER(C.c_int32)]),
     "pt_display_download": (C.c_int, [_R, _FP]),
+    "pt_model_load_gltf": (C.c_int, [C.c_char_p, pt_image_decode_fn, C.c_void_p, C.POINTER(_M)]),
+    "pt_model_scene": (C.POINTER(pt_scene), [_M]),
+    "pt_model_mesh_name": (C.c_char_p, [_M, C.c_int32]),
+    "pt_model_destroy": (C.c_int, [_M]),
+    "pt_model_last_error": (C.c_char_p, []),
+    "pt_image_decode_png": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                      C.c_void_p]),
     "pt_image_write_exr": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),
     "pt_image_write_bmp": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),
     "pt_image_write_pfm": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),

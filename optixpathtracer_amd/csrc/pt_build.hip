@@ -65,10 +65,10 @@ __global__ void k_morton(const float4* tri, int n, float3 cmin, float3 cinv, uin
     vals[i] = (uint32_t)i;
 }
 
-// Leaf-order gather.  isect: v0|orig, (v1-v0)|material, (v2-v0)|0 — the edge subtraction
+// Leaf-order gather.  isect: v0|orig, (v1-v0)|material, (v2-v0)|alpha flag — the edge subtraction
 // is the same single fp32 op the oracle performs, so the hit arithmetic stays identical.
-__global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const uint32_t* order, int n,
-                         float4* isect, float4* shade, float4* st0) {
+__global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const float4* uv_orig, const uint32_t* order,
+                         int n, float4* isect, float4* shade, float4* tuv, float4* st0) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     int i = (int)order[k];
@@ -76,7 +76,11 @@ __global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const u
     const float4 na = nrm_orig[3 * i], nb = nrm_orig[3 * i + 1], nc = nrm_orig[3 * i + 2];
     isect[3 * k] = a;
     isect[3 * k + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w);
-    isect[3 * k + 2] = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.0f);
+    isect[3 * k + 2] = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, c.w);  // w: alpha-cut-out flag
+    if (tuv) {
+        tuv[2 * k] = uv_orig[2 * i];
+        tuv[2 * k + 1] = uv_orig[2 * i + 1];
+    }
     shade[4 * k] = make_float4(b.x, b.y, b.z, na.x);
     shade[4 * k + 1] = make_float4(c.x, c.y, c.z, na.y);
     shade[4 * k + 2] = make_float4(na.z, nb.x, nb.y, nb.z);
@@ -459,8 +463,8 @@ hipError_t ploc_build(const BuildInput& in, const uint32_t* morton_order, BuildO
             c ^= 1;
         }
     }
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig, dfs, n,
-                       out.isect, out.shade, leafbox);
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig, in.uv_orig, dfs,
+                       n, out.isect, out.shade, out.tuv, leafbox);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     B.child = bchild;
     B.range = brange;
@@ -534,7 +538,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             PT_TRY(ploc_build(in, vals2, out, stream, B, root, owned));
         } else {
             hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig,
-                               vals2, n, out.isect, out.shade, st);
+                               in.uv_orig, vals2, n, out.isect, out.shade, out.tuv, st);
             PT_TRY(hipGetLastError());
             table.n = n;
             table.level[0] = st;

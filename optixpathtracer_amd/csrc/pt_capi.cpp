@@ -108,6 +108,9 @@ struct pt_renderer {
     int kernel = PT_KERNEL_MEGA;
     uint32_t frame_id = 0;
     // buffers
+    float4* d_tuv = nullptr;       // per-triangle texcoords (leaf order), textured scenes only
+    uint32_t* d_texels = nullptr;  // RGBA8 texel pool
+    int4* d_texinfo = nullptr;     // per texture: offset, width, height
     float* d_frame = nullptr;   // 1-spp frame (pt_render)
     float* d_display = nullptr;  // progressive view buffer (pt_display_*)
     int display_max = -1;
@@ -138,6 +141,9 @@ struct pt_renderer {
         S.isect = d_isect;
         S.shade = d_shade;
         S.mats = d_mats;
+        S.tuv = d_tuv;
+        S.texels = d_texels;
+        S.texinfo = d_texinfo;
         S.ntri = ntri;
         return S;
     }
@@ -278,14 +284,42 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         ntri += (size_t)me.n_triangles;
     }
     if (ntri > (size_t)0x3fffffff) return fail(PT_ERR_INVALID, "pt_create: too many triangles");
-    std::vector<float4> tri(3 * ntri), nrm(3 * ntri);
-    std::vector<float4> mats(2 * (size_t)std::max(1, scene->n_meshes));
+    // textures (CreateTextures, OptixRenderer.cpp:562-612): one RGBA8 texel pool + (offset, w, h)
+    const int ntex = scene->n_textures;
+    if (ntex < 0 || (ntex > 0 && !scene->textures)) return fail(PT_ERR_INVALID, "pt_create: invalid textures");
+    std::vector<int4> texinfo((size_t)std::max(1, ntex));
+    size_t ntexel = 0;
+    for (int k = 0; k < ntex; ++k) {
+        const pt_texture& tx = scene->textures[k];
+        if (tx.width <= 0 || tx.height <= 0 || !tx.rgba8) return fail(PT_ERR_INVALID, "pt_create: invalid texture");
+        texinfo[(size_t)k] = make_int4((int)ntexel, tx.width, tx.height, 0);
+        ntexel += (size_t)tx.width * (size_t)tx.height;
+    }
+    if (ntexel > (size_t)0x7fffffff) return fail(PT_ERR_INVALID, "pt_create: textures too large");
+    bool any_tex = false;
+    for (int m = 0; m < scene->n_meshes; ++m) {
+        const pt_mesh& me = scene->meshes[m];
+        for (int id : {me.albedo_tex, me.normal_tex, me.metal_rough_tex}) {
+            if (id < -1 || id >= ntex) return fail(PT_ERR_INVALID, "pt_create: texture id out of range");
+            any_tex = any_tex || id >= 0;
+        }
+    }
+    std::vector<float4> tri(3 * ntri), nrm(3 * ntri), uvs(any_tex ? 2 * ntri : 0);
+    std::vector<float4> mats((size_t)kMatStride * (size_t)std::max(1, scene->n_meshes));
     float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
     size_t t = 0;
     for (int m = 0; m < scene->n_meshes; ++m) {
         const pt_mesh& me = scene->meshes[m];
-        mats[2 * m] = make_float4(me.albedo[0], me.albedo[1], me.albedo[2], me.metallic);
-        mats[2 * m + 1] = make_float4(me.roughness, me.normals ? 1.0f : 0.0f, 0.0f, 0.0f);
+        auto ibits = [](int v) {
+            float f;
+            std::memcpy(&f, &v, 4);
+            return f;
+        };
+        const bool textured = me.albedo_tex >= 0 || me.normal_tex >= 0 || me.metal_rough_tex >= 0;
+        mats[kMatStride * m] = make_float4(me.albedo[0], me.albedo[1], me.albedo[2], me.metallic);
+        mats[kMatStride * m + 1] =
+            make_float4(me.roughness, me.normals ? 1.0f : 0.0f, ibits(me.albedo_tex), ibits(me.normal_tex));
+        mats[kMatStride * m + 2] = make_float4(ibits(me.metal_rough_tex), textured ? 1.0f : 0.0f, 0.0f, 0.0f);
         // world-space vertices (modelMatrix * vec4(v,1)); normals pre-transformed with w = 0
         std::vector<float> wv(3 * (size_t)me.n_vertices), wn(3 * (size_t)me.n_vertices, 0.0f);
         for (int v = 0; v < me.n_vertices; ++v) {
@@ -304,11 +338,17 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         }
         for (int i = 0; i < me.n_triangles; ++i, ++t) {
             float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            float uv[6] = {0, 0, 0, 0, 0, 0};  // Mesh::texCoord, zeros when absent (Mesh.cpp:50-53)
             for (int k = 0; k < 3; ++k) {
                 int vi = me.indices[3 * i + k];
                 if (vi < 0 || vi >= me.n_vertices) return fail(PT_ERR_INVALID, "pt_create: index out of range");
+                if (me.texcoords) {
+                    uv[2 * k] = me.texcoords[2 * vi];
+                    uv[2 * k + 1] = me.texcoords[2 * vi + 1];
+                }
                 float wbits;
-                int tag = (k == 0) ? (int)t : (k == 1 ? m : 0);
+                // w tags: v0 = original triangle index, v1 = mesh, v2 = alpha cut-out flag
+                int tag = (k == 0) ? (int)t : (k == 1 ? m : (me.albedo_tex >= 0 ? 1 : 0));
                 std::memcpy(&wbits, &tag, 4);
                 tri[3 * t + k] = make_float4(wv[3 * vi], wv[3 * vi + 1], wv[3 * vi + 2], wbits);
                 nrm[3 * t + k] = make_float4(wn[3 * vi], wn[3 * vi + 1], wn[3 * vi + 2], 0.0f);
@@ -321,6 +361,10 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
                 float c = 0.5f * (lo[a] + hi[a]);
                 cmin[a] = std::min(cmin[a], c);
                 cmax[a] = std::max(cmax[a], c);
+            }
+            if (any_tex) {
+                uvs[2 * t] = make_float4(uv[0], uv[1], uv[2], uv[3]);
+                uvs[2 * t + 1] = make_float4(uv[4], uv[5], 0.0f, 0.0f);
             }
         }
     }
@@ -346,8 +390,28 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     PT_HIPC(hipMalloc(&r->d_mats, sizeof(float4) * mats.size()), "hipMalloc mats");
     PT_HIPC(hipMemcpyAsync(r->d_mats, mats.data(), sizeof(float4) * mats.size(), hipMemcpyHostToDevice, r->stream),
             "upload mats");
+    if (ntex > 0) {
+        PT_HIPC(hipMalloc(&r->d_texinfo, sizeof(int4) * (size_t)ntex), "hipMalloc texinfo");
+        PT_HIPC(hipMemcpyAsync(r->d_texinfo, texinfo.data(), sizeof(int4) * (size_t)ntex, hipMemcpyHostToDevice,
+                               r->stream),
+                "upload texinfo");
+        PT_HIPC(hipMalloc(&r->d_texels, sizeof(uint32_t) * ntexel), "hipMalloc texels");
+        for (int k = 0; k < ntex; ++k) {
+            const pt_texture& tx = scene->textures[k];
+            PT_HIPC(hipMemcpy(r->d_texels + texinfo[(size_t)k].x, tx.rgba8,
+                              sizeof(uint32_t) * (size_t)tx.width * (size_t)tx.height, hipMemcpyHostToDevice),
+                    "upload texels");
+        }
+    }
     if (ntri > 0) {
-        float4 *d_tri_orig = nullptr, *d_nrm_orig = nullptr;
+        float4 *d_tri_orig = nullptr, *d_nrm_orig = nullptr, *d_uv_orig = nullptr;
+        if (any_tex) {
+            PT_HIPC(hipMalloc(&r->d_tuv, sizeof(float4) * 2 * ntri), "hipMalloc tuv");
+            PT_HIPC(hipMalloc(&d_uv_orig, sizeof(float4) * 2 * ntri), "hipMalloc uv_orig");
+            PT_HIPC(hipMemcpyAsync(d_uv_orig, uvs.data(), sizeof(float4) * 2 * ntri, hipMemcpyHostToDevice,
+                                   r->stream),
+                    "upload uv");
+        }
         PT_HIPC(hipMalloc(&r->d_isect, sizeof(float4) * 3 * ntri), "hipMalloc isect");
         PT_HIPC(hipMalloc(&r->d_shade, sizeof(float4) * 4 * ntri), "hipMalloc shade");
         PT_HIPC(hipMalloc(&r->d_nodes, sizeof(BNode4) * std::max<size_t>(1, ntri)), "hipMalloc nodes");
@@ -360,6 +424,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         BuildInput in;
         in.tri_orig = d_tri_orig;
         in.nrm_orig = d_nrm_orig;
+        in.uv_orig = d_uv_orig;
         in.n = (int)ntri;
         in.builder = opt.bvh_builder == PT_BVH_LBVH ? kBuilderLBVH : kBuilderPLOC;
         for (int a = 0; a < 3; ++a) {
@@ -370,11 +435,13 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         bo.nodes = r->d_nodes;
         bo.isect = r->d_isect;
         bo.shade = r->d_shade;
+        bo.tuv = r->d_tuv;
         float ms = 0.0f;
         hipError_t be = lbvh_build(in, bo, r->stream, &ms);
         (void)hipStreamSynchronize(r->stream);
         (void)hipFree(d_tri_orig);
         (void)hipFree(d_nrm_orig);
+        if (d_uv_orig) (void)hipFree(d_uv_orig);
         if (be != hipSuccess) return cleanup_fail(hip_fail(be, "lbvh_build"));
         r->bvh_ms = ms;
         r->bvh_nodes = bo.n_nodes;
@@ -394,6 +461,9 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_isect) (void)hipFree(r->d_isect);
     if (r->d_shade) (void)hipFree(r->d_shade);
     if (r->d_mats) (void)hipFree(r->d_mats);
+    if (r->d_tuv) (void)hipFree(r->d_tuv);
+    if (r->d_texels) (void)hipFree(r->d_texels);
+    if (r->d_texinfo) (void)hipFree(r->d_texinfo);
     if (r->d_lights) (void)hipFree(r->d_lights);
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->d_accum) (void)hipFree(r->d_accum);

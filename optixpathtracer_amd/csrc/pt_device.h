@@ -37,9 +37,17 @@ struct DevScene {
     const BNode4* nodes;
     const float4* isect;
     const float4* shade;
-    const float4* mats;
+    const float4* mats;      // kMatStride per mesh
+    const float4* tuv;       // 2 per triangle (uv0, uv1 | uv2, 0), leaf order; NULL without textures
+    const uint32_t* texels;  // all textures' RGBA8 texels, concatenated
+    const int4* texinfo;     // per texture: texel offset, width, height, 0
     int ntri;
 };
+
+// Material record (3 x float4 per mesh):
+//   [0] albedo.rgb | metallic     [1] roughness | has_normals | albedo_tex | normal_tex
+//   [2] metal_rough_tex | any texture | 0 | 0          (texture ids as int bits, -1 = none)
+constexpr int kMatStride = 3;
 
 struct DevLight {
     float px, py, pz, cr, cg, cb;
@@ -124,6 +132,64 @@ constexpr int kSpillDepth = 64;  // spill + LDS hold a BVH4 path of depth > 20
 #define PT_TRI_PER_STEP 1
 #endif
 
+// ---- textures: devicePrograms.cu:62-73 (SRGB8ToLinear), :131-166 (GetTextureCoord,
+// SampleTextures), :518-543 (AlphaCutout); CreateTextures (OptixRenderer.cpp:562-612) sets up
+// bilinear / wrap / normalized-coordinate / normalized-float uchar4 textures.  Filtering is
+// done here in software with the CUDA texture-fetch formula (filter weight in 1.8 fixed
+// point), the same expression as the oracle's orc_tex_sample, instead of the texture unit
+// whose filter precision is not specified bit for bit.
+__device__ __forceinline__ float srgb_to_linear(float c) {
+    const float m = (c < 0.04045f) ? 0.0f : 1.0f;  // glm::step
+    const float a = c / 12.92f;
+    const float b = powf((c + 0.055f) / 1.055f, 2.4f);  // SavePow
+    return a * (1.0f - m) + b * m;                      // SaveMix
+}
+__device__ __forceinline__ int wrapi(int i, int n) {
+    const int r = i % n;
+    return r < 0 ? r + n : r;
+}
+__device__ __forceinline__ float4 tex_sample(const DevScene& S, int tex, float x, float y, bool srgb) {
+    const int4 ti = S.texinfo[tex];
+    const int W = ti.y, H = ti.z;
+    x = x - floorf(x);
+    y = y - floorf(y);
+    const float xb = x * (float)W - 0.5f, yb = y * (float)H - 0.5f;
+    const float fx = floorf(xb), fy = floorf(yb);
+    const float ax = rintf((xb - fx) * 256.0f) * (1.0f / 256.0f);
+    const float ay = rintf((yb - fy) * 256.0f) * (1.0f / 256.0f);
+    const int i0 = wrapi((int)fx, W), i1 = wrapi((int)fx + 1, W);
+    const int j0 = wrapi((int)fy, H), j1 = wrapi((int)fy + 1, H);
+    const uint32_t* px = S.texels + ti.x;
+    const uint32_t p00 = px[(size_t)j0 * W + i0], p10 = px[(size_t)j0 * W + i1];
+    const uint32_t p01 = px[(size_t)j1 * W + i0], p11 = px[(size_t)j1 * W + i1];
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float t00 = (float)((p00 >> (8 * c)) & 0xff) / 255.0f, t10 = (float)((p10 >> (8 * c)) & 0xff) / 255.0f;
+        const float t01 = (float)((p01 >> (8 * c)) & 0xff) / 255.0f, t11 = (float)((p11 >> (8 * c)) & 0xff) / 255.0f;
+        const float r0 = t00 * (1.0f - ax) + t10 * ax;
+        const float r1 = t01 * (1.0f - ax) + t11 * ax;
+        const float v = r0 * (1.0f - ay) + r1 * ay;
+        o[c] = srgb ? srgb_to_linear(v) : v;
+    }
+    return make_float4(o[0], o[1], o[2], o[3]);
+}
+// GetTextureCoord: (1-u-v)*uv0 + u*uv1 + v*uv2 (zeros when the mesh has no texcoords)
+__device__ __forceinline__ void tri_texcoord(const DevScene& S, int ti, float u, float v, float& x, float& y) {
+    const float4 a = S.tuv[2 * ti], b = S.tuv[2 * ti + 1];
+    const float w = 1.0f - u - v;
+    x = (w * a.x + u * a.z) + v * b.x;
+    y = (w * a.y + u * a.w) + v * b.y;
+}
+// AlphaCutout: a hit on an albedo-textured mesh is ignored when the decoded alpha < 0.9
+// (__anyhit__radiance / __anyhit__shadow, devicePrograms.cu:545-561).
+__device__ __forceinline__ bool alpha_cut(const DevScene& S, int ti, int mi, float u, float v) {
+    const int at = __float_as_int(S.mats[kMatStride * mi + 1].z);
+    float x, y;
+    tri_texcoord(S, ti, u, v, x, y);
+    return tex_sample(S, at, x, y, true).w < 0.9f;
+}
+
 // ---- BVH4 traversal -----------------------------------------------------------------------
 // A per-lane state machine: one step is one inner node (4 slab tests, sorted push of the
 // far hits, descend) or one leaf (<= kLeafMax triangles).  traverse() loops it for one ray;
@@ -203,7 +269,7 @@ __device__ __forceinline__ void stack_refill(TravState& s, int* __restrict__ stk
 
 // Returns true when the ray is finished.  `spill` holds stack entries beyond the LDS
 // depth (never reached on the benchmark scenes; see the overflow counter).
-template <bool ANY, bool STATS, int DEPTH>
+template <bool ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                           int* spill, TravStats& ts) {
     if (s.cur >= 0) {
@@ -265,7 +331,8 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
             const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
             float t, u, v;
             bool bk;
-            const bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
+            bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
+            if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
             const int oi = __float_as_int(A.w);
             if (ANY) {
                 if (hit) {
@@ -301,7 +368,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
 }
 
 // Whole traversal of one ray (megakernel, k_trace).
-template <bool ANY, bool STATS, int DEPTH>
+template <bool ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h,
                                          int* __restrict__ stk, int stride, TravStats& ts) {
     if (STATS) ts.rays++;
@@ -309,7 +376,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tm
     trav_init(s, o, d, tmin, tmax);
     if (S.ntri > 0) {
         int spill[kSpillDepth];
-        while (!trav_step<ANY, STATS, DEPTH>(S, s, stk, stride, spill, ts)) {
+        while (!trav_step<ANY, STATS, DEPTH, TEX>(S, s, stk, stride, spill, ts)) {
         }
     }
     h = s.h;
@@ -332,7 +399,9 @@ __device__ __forceinline__ void camera_ray(const DevLaunch& L, int x, int y, f3&
 }
 
 // Surface reconstruction at a hit: GetNormal / GetSurfacePos (devicePrograms.cu:83-129),
-// back-face flip (:379-382), BuildTangentSpace (:168-212).
+// back-face flip (:379-382), SampleTextures + normal mapping (:392-409), BuildTangentSpace
+// (:168-212).  The texture ids are used as given (the reference's hasNormalTexture /
+// hasMetalRoughTexture = HasAlbedoTex() flag bug, OptixRenderer.cpp:535,540, is not kept).
 struct SurfaceHit {
     f3 pos, ng;
     Frame fr;
@@ -341,12 +410,47 @@ struct SurfaceHit {
     float metallic, roughness;
 };
 
+__device__ __forceinline__ void apply_textures(const DevScene& S, int ti, float u, float v, const float4 M1,
+                                               const float4 M2, f3& albedo, float& metallic, float& roughness,
+                                               f3& Ns) {
+    const int at = __float_as_int(M1.z), nt = __float_as_int(M1.w), mt = __float_as_int(M2.x);
+    float x, y;
+    tri_texcoord(S, ti, u, v, x, y);
+    f3 ntex = mk(0.0f, 0.0f, 0.0f);
+    if (at >= 0) {
+        const float4 c = tex_sample(S, at, x, y, true);
+        albedo = albedo * mk(c.x, c.y, c.z);
+    }
+    if (nt >= 0) {
+        const float4 c = tex_sample(S, nt, x, y, false);
+        ntex = mk(c.x, c.y, c.z);
+    }
+    if (mt >= 0) {
+        const float4 c = tex_sample(S, mt, x, y, false);
+        metallic = c.x;
+        roughness = c.y;
+    }
+    if (ntex.x != 0.0f || ntex.y != 0.0f || ntex.z != 0.0f) {  // normal mapping in the a8 frame of Ns
+        f3 d1 = cross(Ns, mk(0.0f, 0.0f, 1.0f));
+        f3 d2 = cross(Ns, mk(0.0f, 1.0f, 0.0f));
+        f3 T0 = (length(d1) > length(d2)) ? d1 : d2;
+        T0 = normalize(T0);
+        const f3 B0 = cross(T0, Ns);
+        const f3 tn = mk(ntex.x * 2.0f - 1.0f, ntex.y * 2.0f - 1.0f, ntex.z * 2.0f - 1.0f);
+        Ns = normalize(mk((T0.x * tn.x + B0.x * tn.y) + Ns.x * tn.z, (T0.y * tn.x + B0.y * tn.y) + Ns.y * tn.z,
+                          (T0.z * tn.x + B0.z * tn.y) + Ns.z * tn.z));
+    }
+}
+
+// TEX: the scene has textures (kernels are instantiated both ways so untextured scenes keep
+// the texture code out of their register budget).
+template <bool TEX>
 __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 d, SurfaceHit& s) {
     const int ti = h.tri;
     const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
     const float4 S0 = S.shade[4 * ti], S1 = S.shade[4 * ti + 1], S2 = S.shade[4 * ti + 2], S3 = S.shade[4 * ti + 3];
     const int mi = __float_as_int(E1.w);
-    const float4 M0 = S.mats[2 * mi], M1 = S.mats[2 * mi + 1];
+    const float4 M0 = S.mats[kMatStride * mi], M1 = S.mats[kMatStride * mi + 1];
     f3 wo_w = normalize(-d);
     f3 v0 = mk(A.x, A.y, A.z), v1 = mk(S0.x, S0.y, S0.z), v2 = mk(S1.x, S1.y, S1.z);
     f3 n0 = mk(S0.w, S1.w, S2.x), n1 = mk(S2.y, S2.z, S2.w), n2 = mk(S3.x, S3.y, S3.z);
@@ -365,6 +469,13 @@ __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 
     }
     s.pos = mk(w * v0.x + u * v1.x + v * v2.x, w * v0.y + u * v1.y + v * v2.y, w * v0.z + u * v1.z + v * v2.z);
     s.ng = Ng;
+    s.albedo = mk(M0.x, M0.y, M0.z);
+    s.metallic = M0.w;
+    s.roughness = M1.x;
+    if (TEX) {
+        const float4 M2 = S.mats[kMatStride * mi + 2];
+        if (M2.y != 0.0f) apply_textures(S, ti, u, v, M1, M2, s.albedo, s.metallic, s.roughness, Ns);
+    }
     f3 c1 = cross(Ns, mk(0.0f, 0.0f, 1.0f));
     f3 c2 = cross(Ns, mk(0.0f, 1.0f, 0.0f));
     f3 T = (length(c1) > length(c2)) ? c1 : c2;
@@ -373,9 +484,6 @@ __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 
     s.fr.b = cross(T, Ns);
     s.fr.n = Ns;
     s.wo = to_local(s.fr, wo_w);
-    s.albedo = mk(M0.x, M0.y, M0.z);
-    s.metallic = M0.w;
-    s.roughness = M1.x;
 }
 
 // Path state of one camera sample (RadianceRayData, RayData.h:5-21).
@@ -403,11 +511,11 @@ __device__ __forceinline__ bool path_alive(const DevLaunch& L, const PathState& 
 
 // One iteration of SamplePath's loop: TraceRadiance + __closesthit__radiance
 // (devicePrograms.cu:343-514) or __miss__radiance (:576-583).  Returns false on a miss.
-template <int MODE, bool STATS, int DEPTH>
+template <int MODE, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch& L, PathState& p, int* stk,
                                              int stride, TravStats& ts) {
     Hit h;
-    bool hit = traverse<false, STATS, DEPTH>(S, p.o, p.d, 0.0f, 100.0f, h, stk, stride, ts);
+    bool hit = traverse<false, STATS, DEPTH, TEX>(S, p.o, p.d, 0.0f, 100.0f, h, stk, stride, ts);
     if (!hit) {
         p.beta = mk(0, 0, 0);
         p.bounce = 100;
@@ -419,7 +527,7 @@ __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch&
         return;
     }
     SurfaceHit sf;
-    reconstruct(S, h, p.d, sf);
+    reconstruct<TEX>(S, h, p.d, sf);
     const bool conductor = rnd(p.seed) < sf.metallic;  // :400
     // NEE (:446-472), Lighting::GetRandomPointLight (LightMethods.h:25-40)
     float P = 0.0f;
@@ -439,7 +547,7 @@ __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch&
         f3 ldn = normalize(ldir);
         f3 so = sf.pos + 1e-3f * sf.ng;
         Hit sh;
-        bool occluded = traverse<true, STATS, DEPTH>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
+        bool occluded = traverse<true, STATS, DEPTH, TEX>(S, so, normalize(ldir), 0.0f, length(ldir), sh, stk, stride, ts);
         f3 lds = to_local(sf.fr, ldn);
         if (!occluded) {
             f3 f = bsdf_f<MODE>(p.seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);

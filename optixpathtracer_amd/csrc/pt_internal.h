@@ -13,6 +13,7 @@ namespace pt {
 struct BuildInput {
     const float4* tri_orig;  // 3 per triangle: v0|orig idx bits, v1|material bits, v2|0
     const float4* nrm_orig;  // 3 per triangle
+    const float4* uv_orig;   // 2 per triangle (uv0, uv1 | uv2, 0) or NULL (no textures)
     int n;
     float cmin[3], cmax[3];  // centroid bounds (Morton quantisation range)
     int builder;             // kBuilderPLOC (default) or kBuilderLBVH
@@ -25,6 +26,7 @@ struct BuildOutput {
     BNode4* nodes;  // capacity max(1, n) nodes
     float4* isect;  // 3n
     float4* shade;  // 4n
+    float4* tuv;    // 2n or NULL
     int n_nodes;    // written by lbvh_build
     int depth;      // BVH4 levels
 };

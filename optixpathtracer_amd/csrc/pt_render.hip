@@ -49,7 +49,7 @@ __device__ __forceinline__ void flush_stats(const DevLaunch& L, uint32_t segs, c
     if (lane == 0 && L.counters) atomicAdd(&L.counters[0], a);
 }
 
-template <int MODE, bool STATS>
+template <int MODE, bool STATS, bool TEX>
 __global__ __launch_bounds__(kBlock, PT_MK_WAVES) void k_render_mega(DevScene S, DevLaunch L) {
     __shared__ int stack[kStack * kBlock];
     const int lane = threadIdx.x & 63;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(kBlock, PT_MK_WAVES) void k_render_mega(DevScene S,
         path_start(p, co, cd, tea16(pix, L.frame_base));  // devicePrograms.cu:631
         while (true) {
             if (path_alive(L, p)) {
-                path_segment<MODE, STATS, kStack>(S, L, p, stk, kBlock, ts);
+                path_segment<MODE, STATS, kStack, TEX>(S, L, p, stk, kBlock, ts);
                 segs++;
                 continue;
             }
@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kBlock, PT_MK_WAVES) void k_render_mega(DevScene S,
     flush_stats<STATS>(L, segs, ts, lane);
 }
 
+template <bool TEX>
 __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays, int n, int* prim, float* th,
                                                   float* uh, float* vh, int* back, int any_hit) {
     __shared__ int stack[kStack * kBlock];
@@ -100,8 +101,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays,
     Hit h;
     TravStats ts;
     int* stk = stack + threadIdx.x;
-    bool hit = any_hit ? traverse<true, false, kStack>(S, o, d, r[6], r[7], h, stk, kBlock, ts)
-                       : traverse<false, false, kStack>(S, o, d, r[6], r[7], h, stk, kBlock, ts);
+    bool hit = any_hit ? traverse<true, false, kStack, TEX>(S, o, d, r[6], r[7], h, stk, kBlock, ts)
+                       : traverse<false, false, kStack, TEX>(S, o, d, r[6], r[7], h, stk, kBlock, ts);
     prim[i] = hit ? h.orig : -1;
     th[i] = hit && !any_hit ? h.t : 0.0f;
     uh[i] = hit && !any_hit ? h.u : 0.0f;
@@ -112,10 +113,17 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays,
 template <int MODE>
 hipError_t launch_mega(const DevScene& S, const DevLaunch& L, bool stats, hipStream_t stream) {
     dim3 grid((unsigned)((L.width + 15) / 16), (unsigned)((L.height + 15) / 16));
-    if (stats)
-        hipLaunchKernelGGL((k_render_mega<MODE, true>), grid, dim3(kBlock), 0, stream, S, L);
-    else
-        hipLaunchKernelGGL((k_render_mega<MODE, false>), grid, dim3(kBlock), 0, stream, S, L);
+    const bool tex = S.texinfo != nullptr;
+    if (tex) {
+        if (stats)
+            hipLaunchKernelGGL((k_render_mega<MODE, true, true>), grid, dim3(kBlock), 0, stream, S, L);
+        else
+            hipLaunchKernelGGL((k_render_mega<MODE, false, true>), grid, dim3(kBlock), 0, stream, S, L);
+    } else if (stats) {
+        hipLaunchKernelGGL((k_render_mega<MODE, true, false>), grid, dim3(kBlock), 0, stream, S, L);
+    } else {
+        hipLaunchKernelGGL((k_render_mega<MODE, false, false>), grid, dim3(kBlock), 0, stream, S, L);
+    }
     return hipGetLastError();
 }
 
@@ -136,7 +144,11 @@ hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, co
 hipError_t launch_trace(const DevScene& S, const float* d_rays, int n, int* d_prim, float* d_thit, float* d_u,
                         float* d_v, int* d_back, int any_hit, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, S, d_rays, n,
+    if (S.texinfo)
+        hipLaunchKernelGGL(k_trace<true>, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, S, d_rays, n,
+                       d_prim, d_thit, d_u, d_v, d_back, any_hit);
+    else
+        hipLaunchKernelGGL(k_trace<false>, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, S, d_rays, n,
                        d_prim, d_thit, d_u, d_v, d_back, any_hit);
     return hipGetLastError();
 }

@@ -123,7 +123,7 @@ __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
 
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.
-template <bool ANY, bool STATS, class Fetch, class Finish>
+template <bool ANY, bool STATS, bool TEX, class Fetch, class Finish>
 __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TravStats& ts, Fetch fetch,
                                             Finish finish) {
     int spill[kSpillDepth];
@@ -148,14 +148,14 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
         }
         next = min(next + __popcll(m), end);
         if (!__any(ri >= 0 ? 1 : 0)) break;
-        if (ri >= 0 && trav_step<ANY, STATS, kStack>(S, st, stk, kBlockWF, spill, ts)) {
+        if (ri >= 0 && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts)) {
             finish(ri, st);
             ri = -1;
         }
     }
 }
 
-template <bool STATS>
+template <bool STATS, bool TEX>
 __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WFState W, int b, unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kQueue);
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
     const float4* rd = W.ray_d[b & 1];
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<false, STATS>(
+    trace_slice<false, STATS, TEX>(
         S, n, stk, ts,
         [&](int ri, TravState& st) {
             const float4 a = ro[ri], c = rd[ri];
@@ -222,7 +222,7 @@ __device__ __forceinline__ bool continue_path(const SurfaceHit& sf, const BSampl
     return next_bounce < max_bounces && length(beta) > 0.00001f;
 }
 
-template <int MODE>
+template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch 
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
-                reconstruct(S, h, d, sf);
+                reconstruct<TEX>(S, h, d, sf);
                 float4 bv = W.beta[path];
                 uint32_t seed = __float_as_uint(bv.w);
                 f3 beta = mk(bv.x, bv.y, bv.z);
@@ -293,12 +293,13 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch 
     }
 }
 
+template <bool TEX>
 __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_add(DevScene S, WFState W, int b) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<true, false>(
+    trace_slice<true, false, TEX>(
         S, n, stk, ts,
         [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_add(DevScene S
         });
 }
 
-template <int MODE>
+template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
             const Hit h = decode_hit(W.hit[i]);
             if (h.tri >= 0) {
                 SurfaceHit sf;
-                reconstruct(S, h, mk(c.x, c.y, c.z), sf);
+                reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
                 float4 bv = W.beta[path];
                 uint32_t seed = __float_as_uint(bv.w);
                 const bool conductor = rnd(seed) < sf.metallic;
@@ -360,12 +361,13 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
     }
 }
 
+template <bool TEX>
 __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S, WFState W, int b) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<true, false>(
+    trace_slice<true, false, TEX>(
         S, n, stk, ts,
         [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S
         [&](int j, const TravState& st) { W.vis[__float_as_int(W.sh_o[j].w)] = st.h.tri >= 0 ? 0 : 1; });
 }
 
-template <int MODE>
+template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_b(DevScene S, DevLaunch L, W
             if (h.tri >= 0) {
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
-                reconstruct(S, h, d, sf);
+                reconstruct<TEX>(S, h, d, sf);
                 float4 bv = W.beta[path];
                 uint32_t seed = __float_as_uint(bv.w);
                 f3 beta = mk(bv.x, bv.y, bv.z);
@@ -468,21 +470,27 @@ dim3 occupancy_grid(K kernel, int cus) {
     return dim3((unsigned)(per_cu * std::max(1, cus)));
 }
 
+template <int MODE, bool TEX>
+hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
+                          hipStream_t stream, int phase) {
+    if (fused) {
+        if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
+            hipLaunchKernelGGL((k_shade_fused<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L,
+                               W, b);
+    } else if (phase == 0) {
+        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b);
+    } else {
+        hipLaunchKernelGGL((k_shade_b<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b);
+    }
+    return hipGetLastError();
+}
+
 template <int MODE>
 hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int cus,
                         int items, hipStream_t stream, int phase) {
-    if (fused) {
-        if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
-            hipLaunchKernelGGL((k_shade_fused<MODE>), item_grid(items, kBlockSh), dim3(kBlockSh),
-                               0, stream, S, L, W, b);
-    } else if (phase == 0) {
-        hipLaunchKernelGGL((k_shade_a<MODE>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream,
-                           S, L, W, b);
-    } else {
-        hipLaunchKernelGGL((k_shade_b<MODE>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream,
-                           S, L, W, b);
-    }
-    return hipGetLastError();
+    (void)cus;
+    return S.texinfo ? launch_shade_t<MODE, true>(fused, S, L, W, b, items, stream, phase)
+                     : launch_shade_t<MODE, false>(fused, S, L, W, b, items, stream, phase);
 }
 
 hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b,
@@ -545,22 +553,41 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     hipLaunchKernelGGL(k_camera, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L, frame);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const bool fused = fused_mode(mode);
+    const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
     for (int b = 0; b < maxb; ++b) {
         if (trace_events && (e = hipEventRecord(trace_events[2 * b], stream)) != hipSuccess) return e;
-        if (stats)
-            hipLaunchKernelGGL(k_extend<true>, occupancy_grid(k_extend<true>, cus), dim3(kBlockWF), 0, stream, S, W,
-                               b, L.counters);
-        else
-            hipLaunchKernelGGL(k_extend<false>, occupancy_grid(k_extend<false>, cus), dim3(kBlockWF), 0, stream, S,
-                               W, b, L.counters);
+        if (tex) {
+            if (stats)
+                hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockWF),
+                                   0, stream, S, W, b, L.counters);
+            else
+                hipLaunchKernelGGL((k_extend<false, true>), occupancy_grid(k_extend<false, true>, cus),
+                                   dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+        } else if (stats) {
+            hipLaunchKernelGGL((k_extend<true, false>), occupancy_grid(k_extend<true, false>, cus), dim3(kBlockWF), 0,
+                               stream, S, W, b, L.counters);
+        } else {
+            hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockWF),
+                               0, stream, S, W, b, L.counters);
+        }
         if (trace_events && (e = hipEventRecord(trace_events[2 * b + 1], stream)) != hipSuccess) return e;
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (fused) {
             if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_shadow_add, occupancy_grid(k_shadow_add, cus), dim3(kBlockWF), 0, stream, S, W, b);
+            if (tex)
+                hipLaunchKernelGGL(k_shadow_add<true>, occupancy_grid(k_shadow_add<true>, cus), dim3(kBlockWF), 0,
+                                   stream, S, W, b);
+            else
+                hipLaunchKernelGGL(k_shadow_add<false>, occupancy_grid(k_shadow_add<false>, cus), dim3(kBlockWF), 0,
+                                   stream, S, W, b);
         } else {
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_shadow_vis, occupancy_grid(k_shadow_vis, cus), dim3(kBlockWF), 0, stream, S, W, b);
+            if (tex)
+                hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0,
+                                   stream, S, W, b);
+            else
+                hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockWF), 0,
+                                   stream, S, W, b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 1)) != hipSuccess) return e;
         }

@@ -51,12 +51,23 @@ class _SceneBinding:
             pm.albedo[:] = [float(x) for x in m.albedo]
             pm.metallic = float(m.metallic)
             pm.roughness = float(m.roughness)
-            pm.albedo_tex = pm.normal_tex = pm.metal_rough_tex = -1
+            pm.albedo_tex = int(getattr(m, "albedo_tex", -1))
+            pm.normal_tex = int(getattr(m, "normal_tex", -1))
+            pm.metal_rough_tex = int(getattr(m, "metal_rough_tex", -1))
+        texs = list(getattr(scene, "textures", []) or [])
+        tarr = (capi.pt_texture * max(1, len(texs)))()
+        for i, t in enumerate(texs):
+            px = np.ascontiguousarray(t, dtype=np.uint32)
+            self.keep.append(px)
+            tarr[i].rgba8 = px.ctypes.data_as(C.POINTER(C.c_uint32))
+            tarr[i].height, tarr[i].width = int(px.shape[0]), int(px.shape[1])
         self.meshes = meshes
+        self.textures = tarr
         self.scene = capi.pt_scene()
         self.scene.meshes = C.cast(meshes, C.POINTER(capi.pt_mesh))
         self.scene.n_meshes = len(scene.meshes)
-        self.scene.n_textures = 0
+        self.scene.textures = C.cast(tarr, C.POINTER(capi.pt_texture))
+        self.scene.n_textures = len(texs)
 
 
 def camera_from_blender(pos, rot, fov_deg: float, width: int, height: int):

@@ -28,6 +28,9 @@ class Mesh:
     metallic: float = 0.0
     roughness: float = 0.5
     name: str = ""
+    albedo_tex: int = -1  # Mesh.h:35-37 texture ids into Scene.textures (-1 = none)
+    normal_tex: int = -1
+    metal_rough_tex: int = -1
 
     @property
     def n_triangles(self) -> int:
@@ -43,6 +46,7 @@ class Scene:
     fov_deg: float = 40.0  # Camera.cpp:7 ("horizontal" FOV, used as fovy)
     material_mode: int = 0
     name: str = ""
+    textures: list = field(default_factory=list)  # Texture.h: (H, W) uint32 RGBA8 arrays
 
     @property
     def n_triangles(self) -> int:
@@ -181,6 +185,53 @@ def tiny_scene(variant: str = "diffuse") -> Scene:
     return sphere_in_box(variant, sphere_segments=12, sphere_rings=6, grid=2)
 
 
+def _rgba(r, g, b, a) -> np.ndarray:
+    r, g, b, a = (np.asarray(x, dtype=np.uint32) for x in (r, g, b, a))
+    return (r | (g << 8) | (b << 16) | (a << 24)).astype(np.uint32)
+
+
+def textured_scene(variant: str = "diffuse", grid: int = 2) -> Scene:
+    """tiny_scene geometry with the texture paths of SURVEY.md a22 / f2 exercised:
+
+    * back wall + floor: sRGB checker albedo texture whose dark cells are cut out (alpha 0,
+      AlphaCutout) and a bump normal map; texcoords span 0..3 (wrap addressing);
+    * spheres: metallic/roughness texture (R = metallic 0/1 stripes, G = roughness ramp) and
+      the normal map; the left wall has an albedo texture but no texcoords (uv = 0).
+    """
+    sc = sphere_in_box(variant, sphere_segments=12, sphere_rings=6, grid=grid)
+    yy, xx = np.mgrid[0:16, 0:16]
+    cell = ((xx // 4) + (yy // 4)) % 2
+    checker = _rgba(np.where(cell, 230, 40), np.where(cell, 200, 90), np.where(cell, 120, 200),
+                    np.where((cell == 0) & ((xx // 4) % 2 == 0), 0, 255))
+    yy, xx = np.mgrid[0:8, 0:8]
+    nx = 0.5 + 0.35 * np.sin(xx * np.pi / 4.0)
+    ny = 0.5 + 0.35 * np.cos(yy * np.pi / 4.0)
+    normal = _rgba(np.round(nx * 255), np.round(ny * 255), np.full_like(xx, 230), np.full_like(xx, 255))
+    metal_rough = _rgba(np.where(xx % 4 < 2, 255, 0), np.round(yy * 255 / 7.0), np.zeros_like(xx),
+                        np.full_like(xx, 255))
+    sc.textures = [checker, normal, metal_rough]
+    for m in sc.meshes:
+        v = m.vertices
+        if m.name in ("back", "floor"):
+            # planar projection of the engine-space vertices, 3 repeats across the wall
+            a, b = (2, 1) if m.name == "back" else (0, 2)  # engine axes spanned by the wall
+            lo_a, hi_a, lo_b, hi_b = v[:, a].min(), v[:, a].max(), v[:, b].min(), v[:, b].max()
+            uv = np.stack([3.0 * (v[:, a] - lo_a) / (hi_a - lo_a), 3.0 * (v[:, b] - lo_b) / (hi_b - lo_b)], axis=1)
+            m.texcoords = uv.astype(np.float32)
+            m.albedo_tex, m.normal_tex = 0, 1
+        elif m.name == "left":
+            m.albedo_tex = 0  # no texcoords: every hit samples uv (0, 0)
+        elif m.name.startswith("sphere"):
+            c = v.mean(axis=0)
+            d = v - c
+            d /= np.linalg.norm(d, axis=1, keepdims=True)
+            uv = np.stack([0.5 + np.arctan2(d[:, 2], d[:, 0]) / (2 * np.pi), 0.5 - np.arcsin(d[:, 1]) / np.pi], axis=1)
+            m.texcoords = uv.astype(np.float32)
+            m.metal_rough_tex, m.normal_tex = 2, 1
+    sc.name = f"textured_{variant}"
+    return sc
+
+
 # ---------------------------------------------------------------------------------------
 # "Sponza-class" procedural atrium (config 5): ~250k triangles, mixed BRDFs.
 # ---------------------------------------------------------------------------------------
@@ -299,6 +350,8 @@ def sponza_class(seed: int = 12345, target_tris: int = 250_000) -> Scene:
 
 
 def make_scene(name: str) -> Scene:
+    if name.startswith("textured_"):
+        return textured_scene(name[len("textured_"):])
     if name.startswith("sphere_box_"):
         return sphere_in_box(name[len("sphere_box_"):])
     if name.startswith("tiny_"):

@@ -32,7 +32,15 @@ class orc_mesh(C.Structure):
         ("albedo", C.c_float * 3),
         ("metallic", C.c_float),
         ("roughness", C.c_float),
+        ("texcoords", _FP),
+        ("albedo_tex", C.c_int32),
+        ("normal_tex", C.c_int32),
+        ("metal_rough_tex", C.c_int32),
     ]
+
+
+class orc_texture(C.Structure):
+    _fields_ = [("rgba8", _UP), ("width", C.c_int32), ("height", C.c_int32)]
 
 
 class orc_launch(C.Structure):
@@ -82,7 +90,9 @@ def load() -> C.CDLL:
     lib.orc_camera_from_blender.argtypes = [_FP, _FP, C.c_float, C.c_int32, C.c_int32, _FP, _FP, _FP]
     lib.orc_camera_ray.argtypes = [C.POINTER(orc_launch), C.c_int32, C.c_int32, _FP, _FP]
     lib.orc_scene_create.restype = C.c_void_p
-    lib.orc_scene_create.argtypes = [C.POINTER(orc_mesh), C.c_int32]
+    lib.orc_scene_create.argtypes = [C.POINTER(orc_mesh), C.c_int32, C.POINTER(orc_texture), C.c_int32]
+    lib.orc_tex_sample.restype = None
+    lib.orc_tex_sample.argtypes = [C.POINTER(orc_texture), C.c_float, C.c_float, C.c_int32, _FP]
     lib.orc_scene_destroy.argtypes = [C.c_void_p]
     lib.orc_scene_triangles.restype = C.c_int32
     lib.orc_scene_triangles.argtypes = [C.c_void_p]
@@ -150,6 +160,15 @@ def camera_from_blender(pos, rot, fov_deg, w, h):
     return p, iv, ip
 
 
+def tex_sample(rgba8: np.ndarray, x: float, y: float, srgb: bool) -> np.ndarray:
+    """tex2D of the reference's texture objects (+ SRGB8ToLinear when srgb)."""
+    px = np.ascontiguousarray(rgba8, dtype=np.uint32)
+    t = orc_texture(px.ctypes.data_as(_UP), px.shape[1], px.shape[0])
+    out = np.zeros(4, np.float32)
+    load().orc_tex_sample(C.byref(t), float(x), float(y), 1 if srgb else 0, fp(out))
+    return out
+
+
 class OracleScene:
     """The CPU restatement of the render path over one scene (product `Scene` objects)."""
 
@@ -174,7 +193,21 @@ class OracleScene:
             arr[i].albedo[:] = [float(x) for x in m.albedo]
             arr[i].metallic = float(m.metallic)
             arr[i].roughness = float(m.roughness)
-        self.h = self.lib.orc_scene_create(arr, len(scene.meshes))
+            if getattr(m, "texcoords", None) is not None:
+                t = _f(m.texcoords)
+                self._keep.append(t)
+                arr[i].texcoords = fp(t)
+            arr[i].albedo_tex = int(getattr(m, "albedo_tex", -1))
+            arr[i].normal_tex = int(getattr(m, "normal_tex", -1))
+            arr[i].metal_rough_tex = int(getattr(m, "metal_rough_tex", -1))
+        texs = list(getattr(scene, "textures", []) or [])
+        tarr = (orc_texture * max(1, len(texs)))()
+        for i, t in enumerate(texs):
+            px = np.ascontiguousarray(t, dtype=np.uint32)
+            self._keep.append(px)
+            tarr[i].rgba8 = px.ctypes.data_as(_UP)
+            tarr[i].height, tarr[i].width = px.shape
+        self.h = self.lib.orc_scene_create(arr, len(scene.meshes), tarr, len(texs))
         self._lights = None
 
     def launch(self, width, height, max_bounces, material_mode=None, lights=None, camera=None):

@@ -849,7 +849,64 @@ struct orc_scene {
     int32_t* order; /* BVH leaf order -> triangle index */
     onode* nodes;
     int32_t nnodes;
+    float* uv;          /* 6 per triangle (uv0, uv1, uv2; zeros when the mesh has none) */
+    int32_t* tex_ids;   /* 3 per mesh: albedo, normal, metal-rough (-1 = none) */
+    orc_texture* tex;   /* copies of the caller's texture descriptors (pixels borrowed) */
+    uint32_t** texpix;  /* owned pixel copies */
+    int32_t ntex;
 };
+
+/* ---- textures: devicePrograms.cu:62-73 (SRGB8ToLinear), :143-166 (SampleTextures),
+ * OptixRenderer.cpp:562-612 (CreateTextures: uchar4, cudaFilterModeLinear,
+ * cudaAddressModeWrap, normalized coords, cudaReadModeNormalizedFloat).  Bilinear filtering
+ * follows the CUDA programming guide's texture-fetch formula with the filter weight held in
+ * 1.8 fixed point (8 fractional bits); the HIP kernels evaluate exactly the same expression. */
+static inline float srgb_to_linear(float c) {
+    float m = (c < 0.04045f) ? 0.0f : 1.0f;  /* glm::step(0.04045, c) */
+    float a = c / 12.92f;
+    float nom = c + 0.055f;
+    float b = powf(nom / 1.055f, 2.4f);       /* SavePow */
+    return a * (1.0f - m) + b * m;            /* SaveMix */
+}
+static inline int wrapi(int i, int n) { int r = i % n; return r < 0 ? r + n : r; }
+void orc_tex_sample(const orc_texture* t, float x, float y, int32_t srgb, float out[4]) {
+    const int W = t->width, H = t->height;
+    x = x - floorf(x);
+    y = y - floorf(y);
+    float xb = x * (float)W - 0.5f, yb = y * (float)H - 0.5f;
+    float fx = floorf(xb), fy = floorf(yb);
+    float ax = rintf((xb - fx) * 256.0f) * (1.0f / 256.0f);
+    float ay = rintf((yb - fy) * 256.0f) * (1.0f / 256.0f);
+    int i0 = wrapi((int)fx, W), i1 = wrapi((int)fx + 1, W);
+    int j0 = wrapi((int)fy, H), j1 = wrapi((int)fy + 1, H);
+    uint32_t p00 = t->rgba8[(size_t)j0 * W + i0], p10 = t->rgba8[(size_t)j0 * W + i1];
+    uint32_t p01 = t->rgba8[(size_t)j1 * W + i0], p11 = t->rgba8[(size_t)j1 * W + i1];
+    for (int c = 0; c < 4; ++c) {
+        float t00 = (float)((p00 >> (8 * c)) & 0xff) / 255.0f, t10 = (float)((p10 >> (8 * c)) & 0xff) / 255.0f;
+        float t01 = (float)((p01 >> (8 * c)) & 0xff) / 255.0f, t11 = (float)((p11 >> (8 * c)) & 0xff) / 255.0f;
+        float r0 = t00 * (1.0f - ax) + t10 * ax;
+        float r1 = t01 * (1.0f - ax) + t11 * ax;
+        float v = r0 * (1.0f - ay) + r1 * ay;
+        out[c] = srgb ? srgb_to_linear(v) : v;
+    }
+}
+/* GetTextureCoord (devicePrograms.cu:131-141) */
+static inline void tri_uv(const orc_scene* s, int t, float u, float v, float* x, float* y) {
+    const float* q = &s->uv[6 * t];
+    float w = 1.0f - u - v;
+    *x = (w * q[0] + u * q[2]) + v * q[4];
+    *y = (w * q[1] + u * q[3]) + v * q[5];
+}
+/* AlphaCutout (devicePrograms.cu:518-543): albedo-textured meshes drop hits with alpha < 0.9 */
+static int alpha_cut(const orc_scene* s, int t, float u, float v) {
+    int m = s->mesh[t];
+    int at = s->tex_ids ? s->tex_ids[3 * m] : -1;
+    if (at < 0) return 0;
+    float x, y, c[4];
+    tri_uv(s, t, u, v, &x, &y);
+    orc_tex_sample(&s->tex[at], x, y, 1, c);
+    return c[3] < 0.9f;
+}
 
 static void tri_bounds(const orc_scene* s, int t, float lo[3], float hi[3]) {
     for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
@@ -903,7 +960,8 @@ static int build_rec(orc_scene* s, int first, int count) {
     return id;
 }
 
-orc_scene* orc_scene_create(const orc_mesh* meshes, int32_t n_meshes) {
+orc_scene* orc_scene_create(const orc_mesh* meshes, int32_t n_meshes, const orc_texture* textures,
+                            int32_t n_textures) {
     orc_scene* s = (orc_scene*)calloc(1, sizeof(orc_scene));
     int ntri = 0;
     for (int m = 0; m < n_meshes; ++m) ntri += meshes[m].n_triangles;
@@ -917,6 +975,19 @@ orc_scene* orc_scene_create(const orc_mesh* meshes, int32_t n_meshes) {
     s->albedo = (v3*)malloc(sizeof(v3) * (size_t)(n_meshes ? n_meshes : 1));
     s->metallic = (float*)malloc(sizeof(float) * (size_t)(n_meshes ? n_meshes : 1));
     s->roughness = (float*)malloc(sizeof(float) * (size_t)(n_meshes ? n_meshes : 1));
+    s->uv = (float*)calloc(6 * (size_t)(ntri ? ntri : 1), sizeof(float));
+    s->tex_ids = (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)(n_meshes ? n_meshes : 1));
+    s->ntex = n_textures > 0 ? n_textures : 0;
+    s->tex = (orc_texture*)calloc((size_t)(s->ntex ? s->ntex : 1), sizeof(orc_texture));
+    s->texpix = (uint32_t**)calloc((size_t)(s->ntex ? s->ntex : 1), sizeof(uint32_t*));
+    for (int k = 0; k < s->ntex; ++k) {
+        size_t n = (size_t)textures[k].width * (size_t)textures[k].height;
+        s->texpix[k] = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+        if (n) memcpy(s->texpix[k], textures[k].rgba8, sizeof(uint32_t) * n);
+        s->tex[k].rgba8 = s->texpix[k];
+        s->tex[k].width = textures[k].width;
+        s->tex[k].height = textures[k].height;
+    }
     int t = 0;
     for (int m = 0; m < n_meshes; ++m) {
         const orc_mesh* me = &meshes[m];
@@ -925,10 +996,18 @@ orc_scene* orc_scene_create(const orc_mesh* meshes, int32_t n_meshes) {
         s->metallic[m] = me->metallic;
         s->roughness[m] = me->roughness;
         s->has_n[m] = me->normals != NULL;
+        int at = me->albedo_tex, nt = me->normal_tex, mt = me->metal_rough_tex;
+        s->tex_ids[3 * m] = (at >= 0 && at < s->ntex) ? at : -1;
+        s->tex_ids[3 * m + 1] = (nt >= 0 && nt < s->ntex) ? nt : -1;
+        s->tex_ids[3 * m + 2] = (mt >= 0 && mt < s->ntex) ? mt : -1;
         for (int i = 0; i < me->n_triangles; ++i, ++t) {
             s->mesh[t] = m;
             for (int k = 0; k < 3; ++k) {
                 int vi = me->indices[3 * i + k];
+                if (me->texcoords) {
+                    s->uv[6 * t + 2 * k] = me->texcoords[2 * vi];
+                    s->uv[6 * t + 2 * k + 1] = me->texcoords[2 * vi + 1];
+                }
                 /* GetVertices (devicePrograms.cu:77-81): modelMatrix * vec4(v, 1) */
                 float in4[4] = {me->vertices[3 * vi], me->vertices[3 * vi + 1], me->vertices[3 * vi + 2], 1.0f};
                 float o4[4];
@@ -952,6 +1031,9 @@ void orc_scene_destroy(orc_scene* s) {
     if (!s) return;
     free(s->v); free(s->n); free(s->has_n); free(s->model); free(s->mesh);
     free(s->albedo); free(s->metallic); free(s->roughness); free(s->order); free(s->nodes);
+    free(s->uv); free(s->tex_ids);
+    for (int k = 0; k < s->ntex; ++k) free(s->texpix[k]);
+    free(s->texpix); free(s->tex);
     free(s);
 }
 int32_t orc_scene_triangles(const orc_scene* s) { return s->ntri; }
@@ -1008,6 +1090,7 @@ static int trace(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int any
                 float tt, uu, vv;
                 int bk;
                 if (!tri_hit(s, t, o, d, tmin, bt, &tt, &uu, &vv, &bk)) continue;
+                if (alpha_cut(s, t, uu, vv)) continue;  /* __anyhit__radiance/shadow */
                 if (anyhit) return t;
                 if (best < 0 || tt < bt || (tt == bt && t < best)) {
                     best = t; bt = tt; bu = uu; bv = vv; bb = bk;
@@ -1080,7 +1163,40 @@ static v3 sample_path(const orc_scene* s, const orc_launch* lp, v3 origin, v3 di
         sf.albedo = s->albedo[m];
         float metallic = s->metallic[m];
         sf.roughness = s->roughness[m];
+        /* SampleTextures :143-166 (each texture by its own id: the reference's
+         * hasNormalTexture/hasMetalRoughTexture = HasAlbedoTex() flag bug, OptixRenderer.cpp:535,540,
+         * is not reproduced) */
+        v3 normalTex = mk(0, 0, 0);
+        const int32_t* tid = &s->tex_ids[3 * m];
+        if (tid[0] >= 0 || tid[1] >= 0 || tid[2] >= 0) {
+            float tx, ty, c[4];
+            tri_uv(s, prim, u, v, &tx, &ty);
+            if (tid[0] >= 0) {
+                orc_tex_sample(&s->tex[tid[0]], tx, ty, 1, c);
+                sf.albedo = mulv(sf.albedo, mk(c[0], c[1], c[2]));
+            }
+            if (tid[1] >= 0) {
+                orc_tex_sample(&s->tex[tid[1]], tx, ty, 0, c);
+                normalTex = mk(c[0], c[1], c[2]);
+            }
+            if (tid[2] >= 0) {
+                orc_tex_sample(&s->tex[tid[2]], tx, ty, 0, c);
+                metallic = c[0];
+                sf.roughness = c[1];
+            }
+        }
         sf.conductor = rnd(&seed) < metallic;  /* :400 */
+        if (!iszero3(normalTex)) {  /* normal mapping :403-409 in the a8 frame of Ns */
+            v3 d1 = cross3(Ns, mk(0.0f, 0.0f, 1.0f));
+            v3 d2 = cross3(Ns, mk(0.0f, 1.0f, 0.0f));
+            v3 T0 = (length3(d1) > length3(d2)) ? d1 : d2;
+            T0 = normalize3(T0);
+            v3 B0 = cross3(T0, Ns);
+            v3 tn = mk(normalTex.x * 2.0f - 1.0f, normalTex.y * 2.0f - 1.0f, normalTex.z * 2.0f - 1.0f);
+            v3 wn = mk((T0.x * tn.x + B0.x * tn.y) + Ns.x * tn.z, (T0.y * tn.x + B0.y * tn.y) + Ns.y * tn.z,
+                       (T0.z * tn.x + B0.z * tn.y) + Ns.z * tn.z);
+            Ns = normalize3(wn);
+        }
         /* GetTBN / BuildTangentSpace :168-212 */
         v3 c1 = cross3(Ns, mk(0.0f, 0.0f, 1.0f));
         v3 c2 = cross3(Ns, mk(0.0f, 1.0f, 0.0f));

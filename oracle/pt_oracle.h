@@ -42,7 +42,16 @@ typedef struct orc_mesh {
     float albedo[3];
     float metallic;
     float roughness;
+    const float* texcoords;  /* n_vertices*2 or NULL (Mesh::texCoord; zeros when absent, Mesh.cpp:50-53) */
+    int32_t albedo_tex;      /* -1 = none (Mesh.h:35-37) */
+    int32_t normal_tex;
+    int32_t metal_rough_tex;
 } orc_mesh;
+
+typedef struct orc_texture {  /* Texture.h:5-12: RGBA8, row 0 first as stored */
+    const uint32_t* rgba8;
+    int32_t width, height;
+} orc_texture;
 
 typedef struct orc_launch {  /* LaunchParams.h:9-28 */
     int32_t width, height;
@@ -81,7 +90,11 @@ void orc_camera_from_blender(const float blender_pos[3], const float blender_rot
 void orc_camera_ray(const orc_launch* lp, int32_t x, int32_t y, float origin[3], float dir[3]);
 
 /* --- scene + traversal --- */
-orc_scene* orc_scene_create(const orc_mesh* meshes, int32_t n_meshes);
+orc_scene* orc_scene_create(const orc_mesh* meshes, int32_t n_meshes, const orc_texture* textures,
+                            int32_t n_textures);
+/* tex2D<float4> of CreateTextures' texture objects (OptixRenderer.cpp:562-612): bilinear,
+ * wrap, normalized coordinates, normalized-float read; sRGB decode optional (SRGB8ToLinear). */
+void orc_tex_sample(const orc_texture* t, float x, float y, int32_t srgb, float out[4]);
 void orc_scene_destroy(orc_scene* s);
 int32_t orc_scene_triangles(const orc_scene* s);
 /* returns global primitive index (meshes concatenated) or -1 */

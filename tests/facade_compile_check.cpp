@@ -30,8 +30,13 @@ struct Mesh {
         return m;
     }
 };
+struct Texture {
+    uint32_t* pixel = nullptr;
+    ivec2 resolution{-1, -1};
+};
 struct Model {
     std::vector<std::unique_ptr<Mesh>> meshes;
+    std::vector<std::unique_ptr<Texture>> textures;
 };
 struct PointLight {
     vec3 position, color;

@@ -89,6 +89,25 @@ def make():
         o.close()
     g["tiny_variants"] = np.array(list(scenes.VARIANTS))
     g["tiny_images"] = np.array(imgs, dtype=np.float32)
+
+    # textured tiny scene: albedo (sRGB, alpha cut-out), normal and
+    # metal-rough maps; Lambert and Default modes
+    timgs = []
+    for v in ("diffuse", "conductor"):
+        sc = scenes.textured_scene(v)
+        o = O.OracleScene(sc)
+        lp = o.launch(32, 24, 4)
+        img, _ = o.render(lp, 1, 4, threads=1)
+        timgs.append(img)
+        o.close()
+    g["textured_variants"] = np.array(["diffuse", "conductor"])
+    g["textured_images"] = np.array(timgs, dtype=np.float32)
+    # texture fetch: (texture, x, y, srgb) -> rgba over the checker texture
+    sc = scenes.textured_scene("diffuse")
+    pts = np.random.default_rng(11).uniform(-2.0, 3.0, size=(64, 2)).astype(np.float32)
+    g["tex_pts"] = pts
+    g["tex_rgba"] = np.array([[O.tex_sample(sc.textures[0], x, y, s) for x, y in pts] for s in (False, True)],
+                             dtype=np.float32)
     return g
 
 

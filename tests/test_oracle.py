@@ -191,3 +191,57 @@ def test_trace_tie_break_is_structure_independent(oracle_lib):
     assert list(back) == [0, 1]
     np.testing.assert_allclose(t, [1, 1])
     o.close()
+
+
+def _tex_numpy(rgba8, x, y):
+    """Independent numpy restatement of the CUDA texture fetch (bilinear, wrap, 1.8 weights)."""
+    H, W = rgba8.shape
+    f32 = np.float32
+    x, y = f32(x), f32(y)
+    x = f32(x - np.floor(x))
+    y = f32(y - np.floor(y))
+    xb, yb = f32(x * f32(W) - f32(0.5)), f32(y * f32(H) - f32(0.5))
+    fx, fy = np.floor(xb), np.floor(yb)
+    ax = f32(np.rint(f32(xb - fx) * f32(256)) * f32(1 / 256))
+    ay = f32(np.rint(f32(yb - fy) * f32(256)) * f32(1 / 256))
+    i0, j0 = int(fx) % W, int(fy) % H
+    i1, j1 = (int(fx) + 1) % W, (int(fy) + 1) % H
+    ch = lambda p: np.array([(int(p) >> (8 * c)) & 255 for c in range(4)], np.float32) / f32(255)  # noqa: E731
+    t00, t10, t01, t11 = ch(rgba8[j0, i0]), ch(rgba8[j0, i1]), ch(rgba8[j1, i0]), ch(rgba8[j1, i1])
+    r0 = t00 * (f32(1) - ax) + t10 * ax
+    r1 = t01 * (f32(1) - ax) + t11 * ax
+    return (r0 * (f32(1) - ay) + r1 * ay).astype(np.float32)
+
+
+def test_texture_fetch_matches_numpy_and_golden(oracle_lib, golden):
+    """tex2D restated (CreateTextures, OptixRenderer.cpp:562-612) and SRGB8ToLinear
+    (devicePrograms.cu:62-73); golden-pinned."""
+    from oracle.oracle import tex_sample
+    from optixpathtracer_amd import scenes
+
+    tex = scenes.textured_scene("diffuse").textures[0]
+    for (x, y), want_lin, want_srgb in zip(golden["tex_pts"], golden["tex_rgba"][0], golden["tex_rgba"][1]):
+        got = tex_sample(tex, x, y, False)
+        np.testing.assert_array_equal(got, want_lin)
+        np.testing.assert_array_equal(got, _tex_numpy(tex, x, y))
+        srgb = tex_sample(tex, x, y, True)
+        np.testing.assert_array_equal(srgb, want_srgb)
+        c = got.astype(np.float64)
+        ref = np.where(c < 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4)
+        np.testing.assert_allclose(srgb, ref, rtol=2e-6, atol=1e-7)
+
+
+def test_golden_textured_images(oracle_lib, golden):
+    from oracle.oracle import OracleScene
+    from optixpathtracer_amd import scenes
+
+    for name, want in zip(golden["textured_variants"], golden["textured_images"]):
+        o = OracleScene(scenes.textured_scene(str(name)))
+        img, _ = o.render(o.launch(32, 24, 4), 1, 4, threads=3)
+        o.close()
+        np.testing.assert_array_equal(img, want)
+        # the textures change the image: cut-outs, albedo and maps all take effect
+        plain = OracleScene(scenes.tiny_scene(str(name)))
+        base, _ = plain.render(plain.launch(32, 24, 4), 1, 4, threads=3)
+        plain.close()
+        assert np.abs(img - base).mean() > 1e-3
