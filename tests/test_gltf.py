@@ -182,3 +182,28 @@ def test_load_gltf_errors(tmp_path):
     bad.write_text("{\"asset\": [1, 2,}")
     with pytest.raises(PTError, match="json"):
         gltf.load_gltf(bad)
+
+
+def test_scene_round_trip_through_gltf(tmp_path):
+    """A textured scene written as glTF loads back with identical geometry, materials (fp32),
+    texture ids, transforms and texels."""
+    from gltf_export import scene_to_gltf
+    from optixpathtracer_amd import scenes
+
+    f = np.float32
+    sc = scenes.textured_scene("conductor")
+    back = gltf.load_gltf(scene_to_gltf(sc, tmp_path))
+    assert [m.name for m in back.meshes] == [m.name for m in sc.meshes]
+    for a, b in zip(sc.meshes, back.meshes):
+        np.testing.assert_array_equal(a.vertices, b.vertices)
+        np.testing.assert_array_equal(a.normals, b.normals)
+        np.testing.assert_array_equal(a.indices, b.indices)
+        assert (a.texcoords is None) == (b.texcoords is None)
+        if a.texcoords is not None:
+            np.testing.assert_array_equal(a.texcoords, b.texcoords)
+        assert (a.albedo_tex, a.normal_tex, a.metal_rough_tex) == (b.albedo_tex, b.normal_tex, b.metal_rough_tex)
+        np.testing.assert_array_equal(np.asarray(a.albedo, f), np.asarray(b.albedo, f))
+        assert f(a.metallic) == f(b.metallic) and f(a.roughness) == f(b.roughness)
+        np.testing.assert_array_equal(np.asarray(a.model, f).ravel(), b.model.ravel())
+    for t0, t1 in zip(sc.textures, back.textures):
+        np.testing.assert_array_equal(t0, t1)
