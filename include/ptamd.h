@@ -222,6 +222,12 @@ int pt_image_read(const char* path, float* rgb, int32_t* width, int32_t* height)
 /* Per-image parity metric of SURVEY.md §8(c): mean over pixels x 3 channels of (a - b)^2,
  * pixels with a NaN channel counted as 0 (as the reference's EXR writer stores them). */
 double pt_image_mse(const float* a, const float* b, int64_t n_pixels);
+/* LDR-FLIP (Andersson et al. 2020; the README's second metric, README.md:42-46) of two linear
+ * RGB images, each clamped to [0,1] and sRGB-encoded first.  pixels_per_degree <= 0 selects
+ * 67 (0.7 m from a 0.7 m wide 3840-px display).  Returns the mean; error_map (optional)
+ * receives the per-pixel values.  Algorithm notes in pt_image.cpp. */
+double pt_image_flip(const float* ref, const float* test, int32_t width, int32_t height, float pixels_per_degree,
+                     float* error_map);
 const char* pt_image_last_error(void);
 
 #ifdef __cplusplus

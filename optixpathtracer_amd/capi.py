@@ -149,6 +149,7 @@ SIGNATURES = {
     "pt_image_write_pfm": (C.c_int, [C.c_char_p, _FP, C.c_int32, C.c_int32]),
     "pt_image_read": (C.c_int, [C.c_char_p, _FP, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "pt_image_mse": (C.c_double, [_FP, _FP, C.c_int64]),
+    "pt_image_flip": (C.c_double, [_FP, _FP, C.c_int32, C.c_int32, C.c_float, _FP]),
     "pt_image_last_error": (C.c_char_p, []),
 }
 

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <utility>
 #include <vector>
@@ -380,3 +381,232 @@ double pt_image_mse(const float* a, const float* b, int64_t n_pixels) {
 }
 
 }  // extern "C"
+
+// ---- FLIP (LDR) ------------------------------------------------------------------------------
+// The README's second image metric ("FLIP vs PBRT-v4", README.md:42-46) is NVIDIA's FLIP
+// (Andersson et al. 2020, "FLIP: A Difference Evaluator for Alternating Images"), computed
+// there with external tools.  This is the published LDR-FLIP algorithm: linear radiance is
+// clamped to [0,1] and sRGB-encoded (the display image), then
+//   colour: sRGB -> linear -> XYZ -> YCxCz, CSF-shaped Gaussian filtering per opponent channel
+//           (constants of the paper), back to linear RGB clamped to [0,1], CIELab with Hunt
+//           adjustment (a, b scaled by L/100), HyAB distance, ^0.7, redistributed with
+//           pc = 0.4 / pt = 0.95 against the green-blue maximum;
+//   feature: edge / point detectors (first / second Gaussian derivatives, sigma = 0.5 * 0.082 *
+//           ppd, positive and negative lobes normalised to 1) on (Y + 16) / 116;
+//   per pixel E = Ec ^ (1 - Ef), Ef = (max(|d edge|, |d point|) / sqrt(2)) ^ 0.5; FLIP = mean E.
+// All filters are separable and evaluated with edge-clamped borders.
+namespace {
+
+struct Img3 {
+    int w, h;
+    std::vector<float> c[3];
+};
+
+void conv_sep(const std::vector<float>& in, std::vector<float>& out, int w, int h, const std::vector<float>& kx,
+              const std::vector<float>& ky) {
+    const int rx = (int)kx.size() / 2, ry = (int)ky.size() / 2;
+    std::vector<float> tmp((size_t)w * h);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            double s = 0.0;
+            for (int k = -rx; k <= rx; ++k) {
+                const int xx = x + k < 0 ? 0 : (x + k >= w ? w - 1 : x + k);
+                s += (double)kx[(size_t)(k + rx)] * in[(size_t)y * w + xx];
+            }
+            tmp[(size_t)y * w + x] = (float)s;
+        }
+    out.assign((size_t)w * h, 0.0f);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            double s = 0.0;
+            for (int k = -ry; k <= ry; ++k) {
+                const int yy = y + k < 0 ? 0 : (y + k >= h ? h - 1 : y + k);
+                s += (double)ky[(size_t)(k + ry)] * tmp[(size_t)yy * w + x];
+            }
+            out[(size_t)y * w + x] = (float)s;
+        }
+}
+
+const double kPi = 3.14159265358979323846;
+// linear RGB <-> XYZ (sRGB primaries, D65), as in the FLIP reference implementation
+const double kRgb2Xyz[3][3] = {{10135552.0 / 24577794.0, 8788810.0 / 24577794.0, 4435075.0 / 24577794.0},
+                               {2613072.0 / 12288897.0, 8788810.0 / 12288897.0, 887015.0 / 12288897.0},
+                               {1425312.0 / 73733382.0, 8788810.0 / 73733382.0, 70074185.0 / 73733382.0}};
+const double kXyz2Rgb[3][3] = {{3.241003275, -1.537398934, -0.498615861},
+                               {-0.969224334, 1.875930071, 0.041554224},
+                               {0.055639423, -0.204011202, 1.057148933}};
+
+void mat3(const double m[3][3], const double in[3], double out[3]) {
+    for (int r = 0; r < 3; ++r) out[r] = m[r][0] * in[0] + m[r][1] * in[1] + m[r][2] * in[2];
+}
+double srgb2lin(double x) { return x > 0.04045 ? std::pow((x + 0.055) / 1.055, 2.4) : x / 12.92; }
+double lin2srgb(double x) { return x > 0.0031308 ? 1.055 * std::pow(x, 1.0 / 2.4) - 0.055 : 12.92 * x; }
+
+void white(double wp[3]) {
+    const double one[3] = {1, 1, 1};
+    mat3(kRgb2Xyz, one, wp);
+}
+void xyz2ycxcz(const double xyz[3], double o[3]) {
+    double wp[3];
+    white(wp);
+    const double x = xyz[0] / wp[0], y = xyz[1] / wp[1], z = xyz[2] / wp[2];
+    o[0] = 116.0 * y - 16.0;
+    o[1] = 500.0 * (x - y);
+    o[2] = 200.0 * (y - z);
+}
+void ycxcz2xyz(const double c[3], double o[3]) {
+    double wp[3];
+    white(wp);
+    const double y = (c[0] + 16.0) / 116.0, x = c[1] / 500.0 + y, z = y - c[2] / 200.0;
+    o[0] = x * wp[0];
+    o[1] = y * wp[1];
+    o[2] = z * wp[2];
+}
+void xyz2lab(const double xyz[3], double o[3]) {
+    double wp[3];
+    white(wp);
+    const double d = 6.0 / 29.0;
+    auto f = [&](double t) { return t > d * d * d ? std::cbrt(t) : t / (3.0 * d * d) + 4.0 / 29.0; };
+    const double fx = f(xyz[0] / wp[0]), fy = f(xyz[1] / wp[1]), fz = f(xyz[2] / wp[2]);
+    o[0] = 116.0 * fy - 16.0;
+    o[1] = 500.0 * (fx - fy);
+    o[2] = 200.0 * (fy - fz);
+}
+// linear RGB -> Hunt-adjusted L*a*b*
+void rgb2hunt(const double rgb[3], double o[3]) {
+    double xyz[3];
+    mat3(kRgb2Xyz, rgb, xyz);
+    xyz2lab(xyz, o);
+    o[1] *= 0.01 * o[0];
+    o[2] *= 0.01 * o[0];
+}
+double hyab(const double a[3], const double b[3]) {
+    return std::fabs(a[0] - b[0]) + std::sqrt((a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]));
+}
+
+// The CSF filter of one opponent channel: a1*sqrt(pi/b1)*exp(-pi^2 d^2/b1) + a2*..., d in degrees,
+// normalised to unit sum.  Each term is a separable Gaussian with sigma^2 = b / (2 pi^2) deg^2.
+void csf_filter(const std::vector<float>& in, std::vector<float>& out, int w, int h, double ppd, double a1,
+                double b1, double a2, double b2, int r) {
+    auto term = [&](double a, double b, std::vector<float>& res, double& mass) {
+        std::vector<float> k((size_t)(2 * r + 1));
+        double s = 0.0;
+        for (int i = -r; i <= r; ++i) {
+            const double dd = (double)i / ppd;
+            const double v = std::exp(-kPi * kPi * dd * dd / b);
+            k[(size_t)(i + r)] = (float)v;
+            s += v;
+        }
+        // 2D term = a*sqrt(pi/b) * g(x) g(y); its total mass = a*sqrt(pi/b) * s^2
+        mass = a * std::sqrt(kPi / b) * s * s;
+        conv_sep(in, res, w, h, k, k);
+        for (float& v : res) v = (float)(v * a * std::sqrt(kPi / b));
+    };
+    std::vector<float> t1, t2;
+    double m1 = 0.0, m2 = 0.0;
+    term(a1, b1, t1, m1);
+    if (a2 != 0.0) term(a2, b2, t2, m2);
+    out.assign(in.size(), 0.0f);
+    const double tot = m1 + m2;
+    for (size_t i = 0; i < in.size(); ++i) out[i] = (float)((t1[i] + (a2 != 0.0 ? t2[i] : 0.0f)) / tot);
+}
+
+void feature_kernels(double ppd, std::vector<float>& g, std::vector<float>& d1, std::vector<float>& d2) {
+    const double sd = 0.5 * 0.082 * ppd;
+    const int r = (int)std::ceil(3.0 * sd);
+    g.assign((size_t)(2 * r + 1), 0.0f);
+    d1 = g;
+    d2 = g;
+    double sg = 0.0, p1 = 0.0, p2 = 0.0, n2 = 0.0;
+    for (int i = -r; i <= r; ++i) {
+        const double gv = std::exp(-(double)i * i / (2.0 * sd * sd));
+        sg += gv;
+        const double a = -(double)i * gv, b = ((double)i * i / (sd * sd) - 1.0) * gv;
+        if (a > 0) p1 += a;
+        if (b > 0) p2 += b;
+        else n2 -= b;
+        g[(size_t)(i + r)] = (float)gv;
+        d1[(size_t)(i + r)] = (float)a;
+        d2[(size_t)(i + r)] = (float)b;
+    }
+    for (size_t i = 0; i < g.size(); ++i) {
+        g[i] = (float)(g[i] / sg);
+        d1[i] = (float)(d1[i] / p1);
+        d2[i] = (float)(d2[i] > 0 ? d2[i] / p2 : d2[i] / n2);
+    }
+}
+
+}  // namespace
+
+extern "C" double pt_image_flip(const float* ref, const float* test, int32_t width, int32_t height,
+                                float pixels_per_degree, float* error_map) {
+    if (!ref || !test || width <= 0 || height <= 0) return -1.0;
+    const int w = width, h = height;
+    const size_t n = (size_t)w * h;
+    const double ppd = pixels_per_degree > 0.0f ? pixels_per_degree : 67.0;
+    // display images: clamp linear radiance to [0,1], sRGB-encode, then the FLIP input transform
+    std::vector<float> ycx[2][3];
+    for (int im = 0; im < 2; ++im) {
+        const float* src = im ? test : ref;
+        for (int c = 0; c < 3; ++c) ycx[im][c].resize(n);
+        for (size_t i = 0; i < n; ++i) {
+            double rgb[3], xyz[3], o[3];
+            for (int c = 0; c < 3; ++c) {
+                double v = src[3 * i + c];
+                v = std::isnan(v) ? 0.0 : (v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
+                rgb[c] = srgb2lin(lin2srgb(v));
+            }
+            mat3(kRgb2Xyz, rgb, xyz);
+            xyz2ycxcz(xyz, o);
+            for (int c = 0; c < 3; ++c) ycx[im][c][i] = (float)o[c];
+        }
+    }
+    // colour pipeline
+    const double bmax = 0.04;  // max scale parameter of the three CSFs
+    const int r = (int)std::ceil(3.0 * std::sqrt(bmax / (2.0 * kPi * kPi)) * ppd);
+    const double csf[3][4] = {{1.0, 0.0047, 0.0, 1e-5}, {1.0, 0.0053, 0.0, 1e-5}, {34.1, 0.04, 13.5, 0.025}};
+    std::vector<float> filt[2][3];
+    for (int im = 0; im < 2; ++im)
+        for (int c = 0; c < 3; ++c)
+            csf_filter(ycx[im][c], filt[im][c], w, h, ppd, csf[c][0], csf[c][1], csf[c][2], csf[c][3], r);
+    double green[3] = {0, 1, 0}, blue[3] = {0, 0, 1}, hg[3], hb[3];
+    rgb2hunt(green, hg);
+    rgb2hunt(blue, hb);
+    const double qc = 0.7, pc = 0.4, pt = 0.95;
+    const double cmax = std::pow(hyab(hg, hb), qc);
+    // feature pipeline on the achromatic channel (Y + 16) / 116
+    std::vector<float> gk, d1, d2;
+    feature_kernels(ppd, gk, d1, d2);
+    std::vector<float> feat[2][4];
+    for (int im = 0; im < 2; ++im) {
+        std::vector<float> yn(n);
+        for (size_t i = 0; i < n; ++i) yn[i] = (float)((ycx[im][0][i] + 16.0) / 116.0);
+        conv_sep(yn, feat[im][0], w, h, d1, gk);  // edge x
+        conv_sep(yn, feat[im][1], w, h, gk, d1);  // edge y
+        conv_sep(yn, feat[im][2], w, h, d2, gk);  // point x
+        conv_sep(yn, feat[im][3], w, h, gk, d2);  // point y
+    }
+    double sum = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+        double lab[2][3];
+        for (int im = 0; im < 2; ++im) {
+            double yc[3] = {filt[im][0][i], filt[im][1][i], filt[im][2][i]}, xyz[3], rgb[3];
+            ycxcz2xyz(yc, xyz);
+            mat3(kXyz2Rgb, xyz, rgb);
+            for (double& v : rgb) v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+            rgb2hunt(rgb, lab[im]);
+        }
+        const double dc = std::pow(hyab(lab[0], lab[1]), qc);
+        const double ec = dc < pc * cmax ? pt / (pc * cmax) * dc : pt + (dc - pc * cmax) / (cmax - pc * cmax) * (1.0 - pt);
+        const double er = std::hypot((double)feat[0][0][i], (double)feat[0][1][i]);
+        const double et = std::hypot((double)feat[1][0][i], (double)feat[1][1][i]);
+        const double pr = std::hypot((double)feat[0][2][i], (double)feat[0][3][i]);
+        const double ptt = std::hypot((double)feat[1][2][i], (double)feat[1][3][i]);
+        const double df = std::max(std::fabs(er - et), std::fabs(pr - ptt));
+        const double ef = std::pow(df / std::sqrt(2.0), 0.5);
+        const double e = std::pow(ec, 1.0 - ef);
+        if (error_map) error_map[i] = (float)e;
+        sum += e;
+    }
+    return sum / (double)n;
+}

@@ -60,3 +60,16 @@ def mse(a: np.ndarray, b: np.ndarray) -> float:
     if x.shape != y.shape:
         raise PTError(f"shape mismatch {x.shape} vs {y.shape}")
     return float(load().pt_image_mse(_ptr(x), _ptr(y), x.shape[0] * x.shape[1]))
+
+
+def flip(reference: np.ndarray, test: np.ndarray, pixels_per_degree: float = 67.0, error_map: bool = False):
+    """LDR-FLIP of two linear images (clamped, sRGB-encoded); mean, and optionally the map."""
+    x, y = _arr(reference), _arr(test)
+    if x.shape != y.shape:
+        raise PTError(f"shape mismatch {x.shape} vs {y.shape}")
+    emap = np.zeros(x.shape[:2], np.float32) if error_map else None
+    v = float(load().pt_image_flip(_ptr(x), _ptr(y), x.shape[1], x.shape[0], float(pixels_per_degree),
+                                   emap.ctypes.data_as(C.POINTER(C.c_float)) if emap is not None else None))
+    if v < 0:
+        raise PTError("pt_image_flip: invalid arguments")
+    return (v, emap) if error_map else v

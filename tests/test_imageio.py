@@ -107,3 +107,96 @@ def test_mse_definition():
     a[1, 1, 2] = np.nan  # a NaN pixel counts as 0 in every channel
     assert imageio.mse(a, b) == pytest.approx((1.0 + 3 * 4.0) / 12.0)
     assert imageio.mse(b, b) == 0.0
+
+
+def _flip_numpy(ref, test, ppd=67.0):
+    """Independent restatement of LDR-FLIP with full 2-D kernels (edge-clamped borders)."""
+    M = np.array([[10135552 / 24577794, 8788810 / 24577794, 4435075 / 24577794],
+                  [2613072 / 12288897, 8788810 / 12288897, 887015 / 12288897],
+                  [1425312 / 73733382, 8788810 / 73733382, 70074185 / 73733382]])
+    Minv = np.array([[3.241003275, -1.537398934, -0.498615861], [-0.969224334, 1.875930071, 0.041554224],
+                     [0.055639423, -0.204011202, 1.057148933]])
+    wp = M @ np.ones(3)
+
+    def s2l(x):
+        return np.where(x > 0.04045, ((x + 0.055) / 1.055) ** 2.4, x / 12.92)
+
+    def l2s(x):
+        return np.where(x > 0.0031308, 1.055 * np.power(np.maximum(x, 0), 1 / 2.4) - 0.055, 12.92 * x)
+
+    def ycx(img):
+        rgb = s2l(l2s(np.clip(np.nan_to_num(img.astype(np.float64)), 0, 1)))
+        xyz = rgb @ M.T / wp
+        return np.stack([116 * xyz[..., 1] - 16, 500 * (xyz[..., 0] - xyz[..., 1]), 200 * (xyz[..., 1] - xyz[..., 2])],
+                        -1)
+
+    def conv(img, k):
+        r = k.shape[0] // 2
+        p = np.pad(img, r, mode="edge")
+        out = np.zeros_like(img)
+        for dy in range(-r, r + 1):
+            for dx in range(-r, r + 1):
+                out += k[dy + r, dx + r] * p[r + dy:r + dy + img.shape[0], r + dx:r + dx + img.shape[1]]
+        return out
+
+    def hunt(rgb):
+        xyz = rgb @ M.T / wp
+        d = 6 / 29
+        f = np.where(xyz > d ** 3, np.cbrt(xyz), xyz / (3 * d * d) + 4 / 29)
+        L = 116 * f[..., 1] - 16
+        return np.stack([L, 0.01 * L * 500 * (f[..., 0] - f[..., 1]), 0.01 * L * 200 * (f[..., 1] - f[..., 2])], -1)
+
+    r = int(np.ceil(3 * np.sqrt(0.04 / (2 * np.pi ** 2)) * ppd))
+    x = np.arange(-r, r + 1) / ppd
+    z = x[None, :] ** 2 + x[:, None] ** 2
+    csf = [(1, 0.0047, 0, 1e-5), (1, 0.0053, 0, 1e-5), (34.1, 0.04, 13.5, 0.025)]
+    ks = []
+    for a1, b1, a2, b2 in csf:
+        g = a1 * np.sqrt(np.pi / b1) * np.exp(-np.pi ** 2 * z / b1) + a2 * np.sqrt(np.pi / b2) * np.exp(-np.pi ** 2 * z / b2)
+        ks.append(g / g.sum())
+    sd = 0.5 * 0.082 * ppd
+    rf = int(np.ceil(3 * sd))
+    xs = np.arange(-rf, rf + 1, dtype=np.float64)
+    X, Y = np.meshgrid(xs, xs)
+    g = np.exp(-(X ** 2 + Y ** 2) / (2 * sd * sd))
+    e = -X * g
+    e = e / e[e > 0].sum()
+    pnt = (X ** 2 / sd ** 2 - 1) * g
+    pnt = np.where(pnt > 0, pnt / pnt[pnt > 0].sum(), pnt / -pnt[pnt < 0].sum())
+    labs, feats = [], []
+    for img in (ref, test):
+        c = ycx(img)
+        f = np.stack([conv(c[..., k], ks[k]) for k in range(3)], -1)
+        yy = (f[..., 0] + 16) / 116
+        xyz = np.stack([f[..., 1] / 500 + yy, yy, yy - f[..., 2] / 200], -1) * wp
+        labs.append(hunt(np.clip(xyz @ Minv.T, 0, 1)))
+        yn = (c[..., 0] + 16) / 116
+        feats.append((np.hypot(conv(yn, e), conv(yn, e.T)), np.hypot(conv(yn, pnt), conv(yn, pnt.T))))
+    hg, hb = hunt(np.array([0.0, 1.0, 0.0])), hunt(np.array([0.0, 0.0, 1.0]))
+    cmax = (abs(hg[0] - hb[0]) + np.hypot(hg[1] - hb[1], hg[2] - hb[2])) ** 0.7
+    d = labs[0] - labs[1]
+    dc = (np.abs(d[..., 0]) + np.hypot(d[..., 1], d[..., 2])) ** 0.7
+    ec = np.where(dc < 0.4 * cmax, 0.95 / (0.4 * cmax) * dc, 0.95 + (dc - 0.4 * cmax) / (cmax - 0.4 * cmax) * 0.05)
+    df = np.maximum(np.abs(feats[0][0] - feats[1][0]), np.abs(feats[0][1] - feats[1][1]))
+    return ec ** (1 - np.sqrt(df / np.sqrt(2)))
+
+
+def test_flip_matches_numpy_restatement():
+    rng = np.random.default_rng(4)
+    ref = rng.uniform(0, 1.2, size=(20, 24, 3)).astype(np.float32)
+    test = np.clip(ref + rng.normal(0, 0.08, ref.shape), 0, 2).astype(np.float32)
+    v, emap = imageio.flip(ref, test, pixels_per_degree=20.0, error_map=True)
+    want = _flip_numpy(ref, test, ppd=20.0)
+    np.testing.assert_allclose(emap, want, rtol=2e-4, atol=2e-5)
+    assert v == pytest.approx(float(want.mean()), rel=1e-4)
+
+
+def test_flip_properties():
+    rng = np.random.default_rng(5)
+    a = rng.uniform(0, 1, size=(32, 40, 3)).astype(np.float32)
+    assert imageio.flip(a, a) == 0.0
+    small = imageio.flip(a, np.clip(a + rng.normal(0, 0.02, a.shape), 0, 1).astype(np.float32))
+    big = imageio.flip(a, np.clip(a + rng.normal(0, 0.2, a.shape), 0, 1).astype(np.float32))
+    assert 0.0 < small < big <= 1.0
+    bw = imageio.flip(np.zeros_like(a), np.ones_like(a))
+    assert 0.9 < bw <= 1.0
