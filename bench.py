@@ -13,9 +13,9 @@ accumulators are summed to rank 0 with one RCCL reduce (torch.distributed "nccl"
 over xGMI).  Per-GPU work is fixed as N grows ("weak" scaling); value = all samples of
 all ranks / max-over-ranks wall time.
 
-Extra fields: `roofline` (HBM roofline of the dominant kernel, the wavefront's closest-hit
-trace k_extend: 48 algorithmic bytes per traced segment, ray read + hit write, over its
-per-launch average measured with one HIP event pair per launch on the library stream;
+Extra fields: `roofline` (HBM roofline of the dominant kernels, the wavefront's trace kernels
+k_extend + k_trace_pair: 48 algorithmic bytes per traced ray, ray read + result write, over
+their per-launch average measured with one HIP event pair per launch on the library stream;
 `pipeline_gbps` is SURVEY.md §8(d)'s whole-path 396 B/segment + 12 B/sample over the render
 time; `traffic` is the PMC HBM bytes per launch from profiles/traffic.json) and
 `cpu_baseline` (the CPU oracle, oracle/, timed on a bounded band of the same workload on the
@@ -36,7 +36,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 BYTES_PER_SEGMENT = 396  # compulsory SoA queue + gather traffic per path segment
 BYTES_PER_SAMPLE = 12  # final fp32 RGB accumulate
-BYTES_PER_TRACE = 48  # k_extend share of the segment bytes: ray read 32 B + hit write 16 B
+BYTES_PER_TRACE = 48  # trace-kernel share per ray: ray record read 32 B + hit / result write 16 B
 
 
 def log(*a):
@@ -169,13 +169,14 @@ def main():
         kernel_s = st["total_render_ms"] / 1e3
         alg_bytes = st["segments"] * BYTES_PER_SEGMENT + st["samples"] * BYTES_PER_SAMPLE
         if st["trace_kernel_launches"] > 0:
-            # wavefront: the dominant kernel is the closest-hit trace k_extend (one launch per
-            # bounce), each launch bracketed by its own HIP event pair on the library stream
-            dom = "k_extend"
+            # wavefront: the dominant kernels are the trace kernels (k_extend for bounce 0,
+            # k_trace_pair = shadow rays of bounce b + extension rays of b+1), each launch
+            # bracketed by its own HIP event pair on the library stream
+            dom = "k_extend+k_trace_pair"
             launches = int(st["trace_kernel_launches"])
-            per_launch_bytes = st["segments"] * BYTES_PER_TRACE / launches
+            per_launch_bytes = st["trace_kernel_rays"] * BYTES_PER_TRACE / launches
             avg_launch_s = st["trace_kernel_ms"] / 1e3 / launches
-            bytes_def = "48 B per traced segment (ray read 32 + hit write 16)"
+            bytes_def = "48 B per traced ray (ray record read 32 + hit / shadow result write 16)"
         else:
             dom = "k_render_mega"
             launches = max(1, int(st["kernel_launches"]))

@@ -105,10 +105,12 @@ typedef struct pt_stats {
     uint64_t tri_tests;
     uint64_t rays;
     uint64_t stack_overflows;
-    /* closest-hit trace kernel of the wavefront path (k_extend), only timed while
-       pt_set_kernel_timing(r, 1): summed per-launch HIP-event time and launch count */
+    /* trace kernels of the wavefront path (k_extend, and k_trace_pair in the fused modes), only
+       timed while pt_set_kernel_timing(r, 1): summed per-launch HIP-event time and launch count */
     double trace_kernel_ms;
     uint64_t trace_kernel_launches;
+    uint64_t shadow_rays;        /* NEE shadow rays traced since pt_stats_reset */
+    uint64_t trace_kernel_rays;  /* rays traced by the timed trace kernels (k_extend, k_trace_pair) */
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -135,7 +137,7 @@ int pt_set_kernel(pt_renderer* r, int32_t kernel);
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames);
 /* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */
 int pt_set_traversal_stats(pt_renderer* r, int32_t enable);
-/* Bracket every wavefront closest-hit trace launch (k_extend) with its own HIP event pair
+/* Bracket every wavefront trace launch (k_extend, k_trace_pair) with its own HIP event pair
  * on the library stream (pt_stats.trace_kernel_ms / trace_kernel_launches).  Off by default. */
 int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
 

@@ -94,6 +94,8 @@ class pt_stats(C.Structure):
         ("stack_overflows", C.c_uint64),
         ("trace_kernel_ms", C.c_double),
         ("trace_kernel_launches", C.c_uint64),
+        ("shadow_rays", C.c_uint64),
+        ("trace_kernel_rays", C.c_uint64),
     ]
 
 

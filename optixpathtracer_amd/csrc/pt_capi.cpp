@@ -218,8 +218,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
             if (rc) return rc;
             const hipEvent_t* tev = nullptr;
             if (r->kernel_timing) {
-                r->tev_frame.resize(2 * (size_t)r->max_bounces);
-                for (int k = 0; k < r->max_bounces; ++k)
+                r->tev_frame.resize(2 * (size_t)(r->max_bounces + 1));  // <= max_bounces + 1 trace launches
+                for (int k = 0; k <= r->max_bounces; ++k)
                     PT_HIP(r->tev.next(&r->tev_frame[2 * k], &r->tev_frame[2 * k + 1]), "hipEventCreate");
                 tev = r->tev_frame.data();
             }
@@ -682,6 +682,8 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->triangles = r->ntri;
     out->trace_kernel_ms = r->trace_ms;
     out->trace_kernel_launches = r->trace_launches;
+    out->shadow_rays = c[5];
+    out->trace_kernel_rays = c[6];
     return PT_OK;
 }
 

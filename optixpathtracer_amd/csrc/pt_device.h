@@ -204,8 +204,13 @@ struct TravState {
     f3 o, d, inv, io;
     float tmin, best;
     int cur, sp, spc;  // current node/leaf, LDS stack depth, entries spilled
+    bool any;          // any-hit ray (only read by kRayMixed traversals)
     Hit h;
 };
+
+// Ray kinds of a traversal (the ANY template argument): closest hit, any hit (shadow rays,
+// stop at the first accepted hit), or mixed queues where TravState::any decides per lane.
+enum { kRayClosest = 0, kRayAny = 1, kRayMixed = 2 };
 
 __device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, float tmax) {
     s.o = o;
@@ -217,6 +222,7 @@ __device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, 
     s.cur = 0;  // root (always an inner node)
     s.sp = 0;
     s.spc = 0;
+    s.any = false;
     s.h.tri = -1;
     s.h.orig = 0x7fffffff;
 }
@@ -269,7 +275,7 @@ __device__ __forceinline__ void stack_refill(TravState& s, int* __restrict__ stk
 
 // Returns true when the ray is finished.  `spill` holds stack entries beyond the LDS
 // depth (never reached on the benchmark scenes; see the overflow counter).
-template <bool ANY, bool STATS, int DEPTH, bool TEX>
+template <int ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                           int* spill, TravStats& ts) {
     if (s.cur >= 0) {
@@ -287,7 +293,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         int c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
         int c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
         int c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
-        if (!ANY || !PT_ANY_UNSORTED) {
+        if (ANY != kRayAny || !PT_ANY_UNSORTED) {
             t0 = c0 != kEmptyChild ? t0 : inf;
             t1 = c1 != kEmptyChild ? t1 : inf;
             t2 = c2 != kEmptyChild ? t2 : inf;
@@ -334,7 +340,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
             bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
             if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
             const int oi = __float_as_int(A.w);
-            if (ANY) {
+            if (ANY == kRayAny || (ANY == kRayMixed && s.any)) {
                 if (hit) {
                     s.h.tri = ti;
                     s.h.orig = oi;
@@ -368,7 +374,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
 }
 
 // Whole traversal of one ray (megakernel, k_trace).
-template <bool ANY, bool STATS, int DEPTH, bool TEX>
+template <int ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h,
                                          int* __restrict__ stk, int stride, TravStats& ts) {
     if (STATS) ts.rays++;

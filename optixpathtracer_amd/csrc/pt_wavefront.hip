@@ -8,11 +8,14 @@
 //   k_camera            : path p = pixel p of the frame; camera ray -> queue 0, state init
 //   per bounce b:
 //     k_extend          : closest hit of queue b (BVH4 traversal, LDS stack) -> hit records
+//                         (fused modes: bounce 0 only; later bounces ride in k_trace_pair)
 //     fused modes (Lambert / Conductor / Dielectric: BRDF eval draws no random numbers):
 //       k_shade_fused   : surface, metallic coin, light pick, f*|cos|, BSDF sample; NEE
 //                         contribution + shadow ray -> shadow queue (only if f != 0);
 //                         continuation ray -> queue b+1 (wave-ballot compaction)
-//       k_shadow_add    : any-hit; unoccluded -> L[path] += contribution
+//       k_trace_pair    : one launch tracing the shadow rays of bounce b (any hit; unoccluded ->
+//                         L[path] += contribution) and the extension rays of bounce b+1
+//                         (closest hit), which start at the same hit points
 //     RNG-coupled modes (Default / Layered: GlossyDiffuse::f consumes the path seed only
 //     when the light is visible, GlossyDiffuse.h:230-343):
 //       k_shade_a       : surface, coin, light pick -> shadow ray queue
@@ -123,7 +126,7 @@ __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
 
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.
-template <bool ANY, bool STATS, bool TEX, class Fetch, class Finish>
+template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
 __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TravStats& ts, Fetch fetch,
                                             Finish finish) {
     int spill[kSpillDepth];
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
     const float4* rd = W.ray_d[b & 1];
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<false, STATS, TEX>(
+    trace_slice<kRayClosest, STATS, TEX>(
         S, n, stk, ts,
         [&](int ri, TravState& st) {
             const float4 a = ro[ri], c = rd[ri];
@@ -175,7 +178,10 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
                             ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
                             : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
         });
-    if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[0], (unsigned long long)n);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
+        atomicAdd(&counters[0], (unsigned long long)n);  // path segments
+        atomicAdd(&counters[6], (unsigned long long)n);  // rays traced by the timed trace kernels
+    }
     if (STATS && counters) {
         unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
         unsigned long long e = wave_sum_u64(ts.overflow);
@@ -293,26 +299,62 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch 
     }
 }
 
-template <bool TEX>
-__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_add(DevScene S, WFState W, int b) {
+// Fused modes: the shadow rays of bounce b and the extension rays of bounce b + 1 start at
+// the same hit points and are independent, so one launch traces both queues (one SIMT tail
+// and one launch instead of two).  Items [0, n_ext) are extension rays (closest hit ->
+// hit records), items [n_ext, n_ext + n_sh) shadow rays (any hit -> deferred NEE add).
+template <bool STATS, bool TEX>
+__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S, WFState W, int b,
+                                                                      unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
-    const int n = *cnt(W, b, kShadowQ);
+    const int n_ext = *cnt(W, b + 1, kQueue);
+    const int n_sh = *cnt(W, b, kShadowQ);
+    const float4* ro = W.ray_o[(b + 1) & 1];
+    const float4* rd = W.ray_d[(b + 1) & 1];
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<true, false, TEX>(
-        S, n, stk, ts,
-        [&](int j, TravState& st) {
-            const float4 a = W.sh_o[j], c = W.sh_d[j];
-            trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
+    trace_slice<kRayMixed, STATS, TEX>(
+        S, n_ext + n_sh, stk, ts,
+        [&](int i, TravState& st) {
+            if (i < n_ext) {
+                const float4 a = ro[i], c = rd[i];
+                trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
+            } else {
+                const int j = i - n_ext;
+                const float4 a = W.sh_o[j], c = W.sh_d[j];
+                trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
+                st.any = true;
+            }
         },
-        [&](int j, const TravState& st) {
-            if (st.h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+        [&](int i, const TravState& st) {
+            const Hit& h = st.h;
+            if (i < n_ext) {
+                W.hit[i] = h.tri >= 0
+                               ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                               : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+            } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+                const int j = i - n_ext;
                 const int path = __float_as_int(W.sh_o[j].w);
                 const float4 k = W.sh_c[j];
-                float4 l = W.L[path];
+                const float4 l = W.L[path];
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
         });
+    if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
+        atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
+        atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
+        atomicAdd(&counters[6], (unsigned long long)(n_ext + n_sh));  // rays of timed trace kernels
+    }
+    if (STATS && counters) {
+        unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
+        unsigned long long e = wave_sum_u64(ts.overflow);
+        if (lane_id() == 0) {
+            atomicAdd(&counters[1], a);
+            atomicAdd(&counters[2], c);
+            atomicAdd(&counters[3], d);
+            atomicAdd(&counters[4], e);
+        }
+    }
 }
 
 template <int MODE, bool TEX>
@@ -362,12 +404,14 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
 }
 
 template <bool TEX>
-__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S, WFState W, int b) {
+__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S, WFState W, int b,
+                                                                      unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kShadowQ);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[5], (unsigned long long)n);
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<true, false, TEX>(
+    trace_slice<kRayAny, false, TEX>(
         S, n, stk, ts,
         [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
@@ -554,8 +598,10 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const bool fused = fused_mode(mode);
     const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
-    for (int b = 0; b < maxb; ++b) {
-        if (trace_events && (e = hipEventRecord(trace_events[2 * b], stream)) != hipSuccess) return e;
+    int timed = 0;                          // trace launches bracketed by trace_events
+    auto extend = [&](int b) -> hipError_t {
+        hipError_t r;
+        if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
         if (tex) {
             if (stats)
                 hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockWF),
@@ -570,28 +616,51 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
             hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockWF),
                                0, stream, S, W, b, L.counters);
         }
-        if (trace_events && (e = hipEventRecord(trace_events[2 * b + 1], stream)) != hipSuccess) return e;
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (fused) {
-            if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
-            if (tex)
-                hipLaunchKernelGGL(k_shadow_add<true>, occupancy_grid(k_shadow_add<true>, cus), dim3(kBlockWF), 0,
-                                   stream, S, W, b);
+        if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
+        ++timed;
+        return hipGetLastError();
+    };
+    auto pair = [&](int b) -> hipError_t {
+        hipError_t r;
+        if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
+        if (tex) {
+            if (stats)
+                hipLaunchKernelGGL((k_trace_pair<true, true>), occupancy_grid(k_trace_pair<true, true>, cus),
+                                   dim3(kBlockWF), 0, stream, S, W, b, L.counters);
             else
-                hipLaunchKernelGGL(k_shadow_add<false>, occupancy_grid(k_shadow_add<false>, cus), dim3(kBlockWF), 0,
-                                   stream, S, W, b);
+                hipLaunchKernelGGL((k_trace_pair<false, true>), occupancy_grid(k_trace_pair<false, true>, cus),
+                                   dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+        } else if (stats) {
+            hipLaunchKernelGGL((k_trace_pair<true, false>), occupancy_grid(k_trace_pair<true, false>, cus),
+                               dim3(kBlockWF), 0, stream, S, W, b, L.counters);
         } else {
+            hipLaunchKernelGGL((k_trace_pair<false, false>), occupancy_grid(k_trace_pair<false, false>, cus),
+                               dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+        }
+        if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
+        ++timed;
+        return hipGetLastError();
+    };
+    if (fused) {
+        // extend(0); then per bounce: shade(b) -> [shadow rays of b + extension rays of b+1]
+        if ((e = extend(0)) != hipSuccess) return e;
+        for (int b = 0; b < maxb; ++b) {
+            if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
+            if ((e = pair(b)) != hipSuccess) return e;
+        }
+    } else {
+        for (int b = 0; b < maxb; ++b) {
+            if ((e = extend(b)) != hipSuccess) return e;
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
             if (tex)
                 hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0,
-                                   stream, S, W, b);
+                                   stream, S, W, b, L.counters);
             else
                 hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockWF), 0,
-                                   stream, S, W, b);
+                                   stream, S, W, b, L.counters);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 1)) != hipSuccess) return e;
         }
-        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_accum, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L);
     return hipGetLastError();

@@ -15,7 +15,8 @@ import json
 import sys
 from pathlib import Path
 
-KERNELS = ("k_render_mega", "k_extend")  # dominant kernel of the megakernel / wavefront path
+# dominant kernels: the megakernel, or the wavefront's trace kernels taken as one group
+GROUPS = {"k_render_mega": ("k_render_mega",), "k_extend+k_trace_pair": ("k_extend", "k_trace_pair")}
 
 
 def counter_rows(d: Path):
@@ -30,9 +31,9 @@ def per_kernel(d: Path, counter: str):
         if row.get("Counter_Name") != counter:
             continue
         name = row["Kernel_Name"]
-        for k in KERNELS:
-            if k in name:
-                vals.setdefault(k, []).append(float(row["Counter_Value"]))
+        for g, members in GROUPS.items():
+            if any(k in name for k in members):
+                vals.setdefault(g, []).append(float(row["Counter_Value"]))
     return vals
 
 
@@ -41,10 +42,13 @@ def kernel_stats(d: Path):
     for f in sorted(d.rglob("*kernel_stats.csv")):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                for k in KERNELS:
-                    if k in row["Name"]:
-                        out[k] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
-                                  "total_ns": float(row["TotalDurationNs"])}
+                for g, members in GROUPS.items():
+                    if any(k in row["Name"] for k in members):
+                        o = out.setdefault(g, {"calls": 0, "total_ns": 0.0})
+                        o["calls"] += int(row["Calls"])
+                        o["total_ns"] += float(row["TotalDurationNs"])
+    for o in out.values():
+        o["avg_ns"] = o["total_ns"] / max(1, o["calls"])
     return out
 
 
@@ -53,7 +57,7 @@ def main():
     fetch = per_kernel(root / "fetch", "FETCH_SIZE")
     write = per_kernel(root / "write", "WRITE_SIZE")
     stats = kernel_stats(root / "kt")
-    kernel = next((k for k in KERNELS if k in fetch and k in write), None)
+    kernel = next((k for k in GROUPS if k in fetch and k in write), None)
     if kernel is None:
         print(json.dumps({"error": "no PMC rows for the render kernels"}))
         return
