@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -133,7 +134,7 @@ struct pt_renderer {
     double last_ms = 0.0, total_ms = 0.0;
     uint64_t calls = 0;
     double bvh_ms = 0.0;
-    int frames_per_launch = 8;
+    int frames_per_launch = 16;
 
     DevScene scene() const {
         DevScene S;
@@ -203,16 +204,23 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
     int kernel = r->kernel;
     if (kernel == PT_KERNEL_AUTO) kernel = PT_KERNEL_WAVEFRONT;
     if (kernel == PT_KERNEL_WAVEFRONT) {
+        // Frames per wavefront launch chain: the queues hold nf frames' paths (168 B each), at most
+        // kMaxWFPaths of them.  Batching amortises launch gaps and the per-kernel SIMT tail:
+        // Lambert 1080p 545 / 648 / 664 Msamples/s at 1 / 8 / 16 frames.
+        constexpr int kMaxWFPaths = 1 << 26;
         const int P = r->width * r->height;
-        if (r->wf.paths != P || r->wf.max_bounces < r->max_bounces) {
+        const int nf_cap = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
+                                                 kMaxWFPaths / std::max(1, P)}));
+        if (r->wf.paths < P * nf_cap || r->wf.max_bounces < r->max_bounces) {
             PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
             wavefront_free(r->wf);
-            PT_HIP(wavefront_alloc(r->wf, P, std::max(1, r->max_bounces)), "wavefront_alloc");
+            PT_HIP(wavefront_alloc(r->wf, P * nf_cap, std::max(1, r->max_bounces)), "wavefront_alloc");
         }
         int dev_cus = 256;
         (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, r->device);
-        for (uint32_t f = 0; f < n; ++f) {  // one event pair per frame (the frame's kernel chain)
-            DevLaunch L = make_launch(r, accum, first + f, 1);
+        for (uint32_t f = 0; f < n;) {  // one event pair per batch (the batch's kernel chain)
+            const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
+            DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf);
             hipEvent_t a, b;
             rc = next_event_pair(r, &a, &b);
             if (rc) return rc;
@@ -224,10 +232,11 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
                 tev = r->tev_frame.data();
             }
             PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
-            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, dev_cus,
+            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, nf, dev_cus,
                                           r->stream, tev),
                    "wavefront launch");
             PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
+            f += (uint32_t)nf;
         }
         done = n;
     }

@@ -5,7 +5,8 @@
 // persistent, grid-stride kernels over SoA queues in HBM, so the traversal kernels carry
 // only a ray (low VGPR count -> high occupancy) and the BSDF code runs in its own kernel:
 //
-//   k_camera            : path p = pixel p of the frame; camera ray -> queue 0, state init
+//   k_camera            : path q = f * P + pixel for the nf frames of the batch; camera ray ->
+//                         queue 0, state init
 //   per bounce b:
 //     k_extend          : closest hit of queue b (BVH4 traversal, LDS stack) -> hit records
 //                         (fused modes: bounce 0 only; later bounces ride in k_trace_pair)
@@ -21,11 +22,11 @@
 //       k_shade_a       : surface, coin, light pick -> shadow ray queue
 //       k_shadow_vis    : any-hit -> vis[path]
 //       k_shade_b       : if visible: f (may draw), NEE; BSDF sample -> queue b+1
-//   k_accum             : accum[pixel] += L[path]   (one frame at a time: same fp32 order as
-//                         the sequential reference accumulation)
+//   k_accum             : accum[pixel] += L[f * P + pixel] for f = 0 .. nf-1 in order (the same
+//                         fp32 order as the sequential reference accumulation)
 //
 // Every kernel reads queue lengths from device memory written by an earlier launch (kernel
-// boundaries order the hand-off), so a whole frame is enqueued without host round trips.
+// boundaries order the hand-off), so a whole batch of frames is enqueued without host round trips.
 #include <unordered_map>
 
 #include "pt_internal.h"
@@ -94,19 +95,23 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     return lds[kWavesSh] + lds[wave] + prefix;
 }
 
-__global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame) {
+// Paths of nf consecutive frames are in flight together (path q = f * P + pixel), so every
+// launch works on nf frames' queues: fewer launches and one SIMT tail per nf frames.
+__global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame0, int nf) {
     const int P = L.width * L.height;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const int Q = P * nf;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += gridDim.x * blockDim.x) {
+        const int f = q / P, p = q - f * P;
         const int x = p % L.width, y = p / L.width;
         f3 o, d;
         camera_ray(L, x, y, o, d);
-        W.ray_o[0][p] = make_float4(o.x, o.y, o.z, __int_as_float(p));
-        W.ray_d[0][p] = make_float4(d.x, d.y, d.z, 0.0f);
-        const uint32_t seed = tea16((uint32_t)(L.width * y + x), frame);  // devicePrograms.cu:631
-        W.beta[p] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(seed));
-        W.L[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        W.ray_o[0][q] = make_float4(o.x, o.y, o.z, __int_as_float(q));
+        W.ray_d[0][q] = make_float4(d.x, d.y, d.z, 0.0f);
+        const uint32_t seed = tea16((uint32_t)(L.width * y + x), frame0 + (uint32_t)f);  // devicePrograms.cu:631
+        W.beta[q] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(seed));
+        W.L[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kQueue) = P;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kQueue) = Q;
 }
 
 // This wave's static slice of a queue of length n (grid sized to residency, so every wave
@@ -480,14 +485,20 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_b(DevScene S, DevLaunch L, W
     }
 }
 
-__global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L) {
+__global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L, int nf) {
     const int P = L.width * L.height;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        const float4 l = W.L[p];
         const size_t idx = (size_t)p * 3;
-        L.accum[idx] += l.x;
-        L.accum[idx + 1] += l.y;
-        L.accum[idx + 2] += l.z;
+        float sx = L.accum[idx], sy = L.accum[idx + 1], sz = L.accum[idx + 2];
+        for (int f = 0; f < nf; ++f) {  // frames in order: the sequential accumulation
+            const float4 l = W.L[(size_t)f * P + p];
+            sx += l.x;
+            sy += l.y;
+            sz += l.z;
+        }
+        L.accum[idx] = sx;
+        L.accum[idx + 1] = sy;
+        L.accum[idx + 2] = sz;
     }
 }
 
@@ -589,12 +600,12 @@ void wavefront_free(WFState& W) {
 }
 
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
-                                  uint32_t frame, int cus, hipStream_t stream, const hipEvent_t* trace_events) {
-    const int P = L.width * L.height;
+                                  uint32_t frame, int nf, int cus, hipStream_t stream, const hipEvent_t* trace_events) {
+    const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_camera, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L, frame);
+    hipLaunchKernelGGL(k_camera, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L, frame, nf);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const bool fused = fused_mode(mode);
     const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
@@ -662,7 +673,7 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 1)) != hipSuccess) return e;
         }
     }
-    hipLaunchKernelGGL(k_accum, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L);
+    hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
     return hipGetLastError();
 }
 

@@ -13,12 +13,15 @@ def image_mse(a: np.ndarray, b: np.ndarray) -> float:
     return float(np.mean((a - b) ** 2))
 
 
-def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, kernel=0, device=0):
+def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, kernel=0, device=0,
+               frames_per_launch=None):
     from optixpathtracer_amd.renderer import setup_renderer
 
     r = setup_renderer(scene, width, height, max_bounces, device=device, kernel=kernel)
     if mode is not None:
         r.set_material_mode(mode)
+    if frames_per_launch is not None:
+        r.set_frames_per_launch(frames_per_launch)
     r.accum_clear()
     r.render_frames(first_frame, n_frames)
     img = r.accum()

@@ -230,6 +230,23 @@ def test_wavefront_bit_identical_to_megakernel(variant):
     assert sa["segments"] == sb["segments"]
 
 
+@pytest.mark.parametrize("mode", [1, 3, 0])
+def test_wavefront_frame_batching_bit_identical(mode):
+    """The wavefront keeps the paths of a batch of frames in flight together (path = f * P +
+    pixel) and k_accum adds the batch's frames in order, so any batch size -- including a
+    ragged last batch (11 frames = 4 + 4 + 3) -- gives the accumulator of one frame at a time."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("diffuse")
+    ref, sr = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=1, frames_per_launch=1)
+    for fpl in (4, 16):
+        img, st = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=1, frames_per_launch=fpl)
+        np.testing.assert_array_equal(img, ref)
+        assert st["segments"] == sr["segments"]
+    mega, _ = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=0)
+    np.testing.assert_array_equal(mega, ref)
+
+
 @pytest.mark.parametrize("mode", [1, 0])
 def test_wavefront_config1_parity(diffuse_scene, mode):
     g, st = gpu_render(diffuse_scene, 256, 256, 4, 1, 16, mode=mode, kernel=1)

@@ -49,7 +49,7 @@ def main():
                     r.set_material_mode(mode)
                     r.set_frames_per_launch(fpl)
                     r.accum_clear()
-                    r.render_frames(1, min(a.spp, 2))  # warm
+                    r.render_frames(1, min(a.spp, fpl))  # warm (also sizes the wavefront queues)
                     r.synchronize()
                     best = None
                     for rep in range(a.repeat):
