@@ -221,7 +221,12 @@ __global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, 
     for (int k = 0; k < 4; ++k) {
         if (k >= n) {
             cc[k] = kEmptyChild;
-            for (int a = 0; a < 3; ++a) lo[a][k] = hi[a][k] = 0.0f;
+            // inverted box: misses for every ray direction (the sign-selected slab test of
+            // pt_device.h node_test relies on it instead of testing the child id)
+            for (int a = 0; a < 3; ++a) {
+                lo[a][k] = __int_as_float(0x7f800000);
+                hi[a][k] = -__int_as_float(0x7f800000);
+            }
             continue;
         }
         float4 l4, h4;

@@ -128,6 +128,9 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
 // The LDS depth is a template parameter (DEPTH): it trades LDS per workgroup against
 // occupancy per kernel (see pt_render.hip / pt_wavefront.hip).
 constexpr int kSpillDepth = 64;  // spill + LDS hold a BVH4 path of depth > 20
+#ifndef PT_DUAL_STEP
+#define PT_DUAL_STEP 1  // one node AND one triangle per traversal step (see trav_step)
+#endif
 #ifndef PT_TRI_PER_STEP
 #define PT_TRI_PER_STEP 1
 #endif
@@ -204,6 +207,8 @@ struct TravState {
     f3 o, d, inv, io;
     float tmin, best;
     int cur, sp, spc;  // current node/leaf, LDS stack depth, entries spilled
+    int leaf;          // PT_DUAL_STEP: leaf whose triangles are tested alongside node steps
+    int nx, ny, nz;    // byte offset (0 or 16) of the near slab plane per axis within the node
     bool any;          // any-hit ray (only read by kRayMixed traversals)
     Hit h;
 };
@@ -217,11 +222,15 @@ __device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, 
     s.d = d;
     s.inv = safe_inv(d);
     s.io = mk(o.x * s.inv.x, o.y * s.inv.y, o.z * s.inv.z);
+    s.nx = s.inv.x < 0.0f ? 16 : 0;
+    s.ny = s.inv.y < 0.0f ? 16 : 0;
+    s.nz = s.inv.z < 0.0f ? 16 : 0;
     s.tmin = tmin;
     s.best = tmax;
     s.cur = 0;  // root (always an inner node)
     s.sp = 0;
     s.spc = 0;
+    s.leaf = kEmptyChild;
     s.any = false;
     s.h.tri = -1;
     s.h.orig = 0x7fffffff;
@@ -276,7 +285,7 @@ __device__ __forceinline__ void stack_refill(TravState& s, int* __restrict__ stk
 // Returns true when the ray is finished.  `spill` holds stack entries beyond the LDS
 // depth (never reached on the benchmark scenes; see the overflow counter).
 template <int ANY, bool STATS, int DEPTH, bool TEX>
-__device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
+__device__ __forceinline__ bool trav_step_single(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                           int* spill, TravStats& ts) {
     if (s.cur >= 0) {
         if (STATS) ts.nodes++;
@@ -371,6 +380,184 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
     --s.sp;
     s.cur = stk[s.sp * stride];
     return false;
+}
+
+#ifndef PT_NODE_SIGNSEL
+#define PT_NODE_SIGNSEL 1
+#endif
+typedef float pt_f2 __attribute__((ext_vector_type(2)));
+
+// Slab test of the four children of node `ni`, hits as (t_near, child) with misses and
+// empty slots as kEmptyChild.  PT_NODE_SIGNSEL: the ray's direction signs pick the near and
+// far plane of every axis at load time (per-lane byte offsets into the node), so each child
+// needs no min/max per axis, and the plane distances are two children per packed v_pk_fma.
+// The planes are the same ones min/max would choose (fma is monotone in the plane
+// coordinate), so the result equals slab()'s.
+__device__ __forceinline__ void node_test(const DevScene& S, const TravState& s, int ni, float& t0, float& t1,
+                                          float& t2, float& t3, int& c0, int& c1, int& c2, int& c3) {
+    bool h0, h1, h2, h3;
+#if PT_NODE_SIGNSEL
+    // raw buffer loads: one 32-bit offset add per plane instead of a 64-bit address
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.nodes, 0, 0x7fffffff, 0x00020000);
+    const int nb = ni << 7;
+    auto ld = [&](int off) {
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + off, 0, 0));
+    };
+    const float4 ax = ld(s.nx), bx = ld(16 - s.nx);
+    const float4 ay = ld(32 + s.ny), by = ld(48 - s.ny);
+    const float4 az = ld(64 + s.nz), bz = ld(80 - s.nz);
+    const int4 ch = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + 96, 0, 0));
+    const pt_f2 ix = {s.inv.x, s.inv.x}, iy = {s.inv.y, s.inv.y}, iz = {s.inv.z, s.inv.z};
+    const pt_f2 ox = {-s.io.x, -s.io.x}, oy = {-s.io.y, -s.io.y}, oz = {-s.io.z, -s.io.z};
+    const pt_f2 nx01 = __builtin_elementwise_fma(pt_f2{ax.x, ax.y}, ix, ox);
+    const pt_f2 nx23 = __builtin_elementwise_fma(pt_f2{ax.z, ax.w}, ix, ox);
+    const pt_f2 fx01 = __builtin_elementwise_fma(pt_f2{bx.x, bx.y}, ix, ox);
+    const pt_f2 fx23 = __builtin_elementwise_fma(pt_f2{bx.z, bx.w}, ix, ox);
+    const pt_f2 ny01 = __builtin_elementwise_fma(pt_f2{ay.x, ay.y}, iy, oy);
+    const pt_f2 ny23 = __builtin_elementwise_fma(pt_f2{ay.z, ay.w}, iy, oy);
+    const pt_f2 fy01 = __builtin_elementwise_fma(pt_f2{by.x, by.y}, iy, oy);
+    const pt_f2 fy23 = __builtin_elementwise_fma(pt_f2{by.z, by.w}, iy, oy);
+    const pt_f2 nz01 = __builtin_elementwise_fma(pt_f2{az.x, az.y}, iz, oz);
+    const pt_f2 nz23 = __builtin_elementwise_fma(pt_f2{az.z, az.w}, iz, oz);
+    const pt_f2 fz01 = __builtin_elementwise_fma(pt_f2{bz.x, bz.y}, iz, oz);
+    const pt_f2 fz23 = __builtin_elementwise_fma(pt_f2{bz.z, bz.w}, iz, oz);
+    const float tmin = s.tmin, tmax = s.best;
+    t0 = fmaxf(fmaxf(nx01.x, ny01.x), fmaxf(nz01.x, tmin));
+    t1 = fmaxf(fmaxf(nx01.y, ny01.y), fmaxf(nz01.y, tmin));
+    t2 = fmaxf(fmaxf(nx23.x, ny23.x), fmaxf(nz23.x, tmin));
+    t3 = fmaxf(fmaxf(nx23.y, ny23.y), fmaxf(nz23.y, tmin));
+    pt_f2 f01 = {fminf(fminf(fx01.x, fy01.x), fminf(fz01.x, tmax)), fminf(fminf(fx01.y, fy01.y), fminf(fz01.y, tmax))};
+    pt_f2 f23 = {fminf(fminf(fx23.x, fy23.x), fminf(fz23.x, tmax)), fminf(fminf(fx23.y, fy23.y), fminf(fz23.y, tmax))};
+    f01 = f01 * pt_f2{1.0000004f, 1.0000004f};
+    f23 = f23 * pt_f2{1.0000004f, 1.0000004f};
+    h0 = t0 <= f01.x;
+    h1 = t1 <= f01.y;
+    h2 = t2 <= f23.x;
+    h3 = t3 <= f23.y;
+    // empty slots hold inverted boxes (pt_build.hip k_collapse): they never hit
+    const float inf = __int_as_float(0x7f800000);
+    t0 = h0 ? t0 : inf;
+    t1 = h1 ? t1 : inf;
+    t2 = h2 ? t2 : inf;
+    t3 = h3 ? t3 : inf;
+    c0 = h0 ? ch.x : kEmptyChild;
+    c1 = h1 ? ch.y : kEmptyChild;
+    c2 = h2 ? ch.z : kEmptyChild;
+    c3 = h3 ? ch.w : kEmptyChild;
+#else
+    const BNode4& n = S.nodes[ni];
+    const int4 ch = n.child;
+    const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
+    t0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, s.inv, s.io, s.tmin, s.best, h0);
+    t1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, s.inv, s.io, s.tmin, s.best, h1);
+    t2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, s.inv, s.io, s.tmin, s.best, h2);
+    t3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, s.inv, s.io, s.tmin, s.best, h3);
+    c0 = (h0 && ch.x != kEmptyChild) ? ch.x : kEmptyChild;
+    c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
+    c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
+    c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
+    const float inf = __int_as_float(0x7f800000);
+    t0 = c0 != kEmptyChild ? t0 : inf;
+    t1 = c1 != kEmptyChild ? t1 : inf;
+    t2 = c2 != kEmptyChild ? t2 : inf;
+    t3 = c3 != kEmptyChild ? t3 : inf;
+#endif
+}
+
+// Test one triangle of the leaf s.leaf and advance it; true when an any-hit ray is done.
+template <int ANY, bool STATS, bool TEX>
+__device__ __forceinline__ bool leaf_tri_step(const DevScene& S, TravState& s, TravStats& ts) {
+    const int first = leaf_first(s.leaf), cnt = leaf_count(s.leaf);
+    const int ti = first;
+    if (STATS) ts.tris++;
+    const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+    float t, u, v;
+    bool bk;
+    bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
+    if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
+    const int oi = __float_as_int(A.w);
+    s.leaf = cnt > 1 ? ~(((first + 1) << 3) | (cnt - 2)) : kEmptyChild;  // rest of the leaf
+    if (ANY == kRayAny || (ANY == kRayMixed && s.any)) {
+        if (hit) {
+            s.h.tri = ti;
+            s.h.orig = oi;
+            return true;
+        }
+    } else {
+        // closest hit ordered by (t, original index): independent of the visiting order
+        const bool take = hit && (t < s.best || oi < s.h.orig);
+        s.best = take ? t : s.best;
+        s.h.t = take ? t : s.h.t;
+        s.h.u = take ? u : s.h.u;
+        s.h.v = take ? v : s.h.v;
+        s.h.back = take ? bk : s.h.back;
+        s.h.tri = take ? ti : s.h.tri;
+        s.h.orig = take ? oi : s.h.orig;
+    }
+    return false;
+}
+
+// Next stack entry into s.cur (kEmptyChild when the stack is empty).
+template <int DEPTH>
+__device__ __forceinline__ void stack_pop(TravState& s, int* __restrict__ stk, int stride, const int* spill) {
+    if (s.sp == 0 && s.spc > 0) stack_refill<DEPTH>(s, stk, stride, spill);
+    const int sp = s.sp - 1;
+    const int e = stk[max(sp, 0) * stride];
+    s.cur = sp >= 0 ? e : kEmptyChild;
+    s.sp = max(sp, 0);
+}
+
+// One traversal step; true when the ray is finished.  `spill` holds stack entries beyond
+// the LDS depth (never reached on the benchmark scenes; see the overflow counter).
+//
+// PT_DUAL_STEP: a lane carries a node (s.cur) and a leaf (s.leaf) at once, and one step
+// tests one triangle of the leaf AND visits the node.  A wave whose lanes are split between
+// nodes and triangles executes both halves of the step anyway; here most lanes do useful
+// work in both, so a ray finishes in ~max(nodes, triangles) steps instead of their sum.
+// Leaves are therefore tested out of front-to-back order, which the (t, index) closest-hit
+// rule makes harmless; culling stays conservative (best only shrinks).
+template <int ANY, bool STATS, int DEPTH, bool TEX>
+__device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
+                                          int* spill, TravStats& ts) {
+#if PT_DUAL_STEP
+    if (s.leaf != kEmptyChild) {
+        if (leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
+    }
+    if (s.cur >= 0) {
+        if (STATS) ts.nodes++;
+        float t0, t1, t2, t3;
+        int c0, c1, c2, c3;
+        node_test(S, s, s.cur, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
+        if (ANY != kRayAny || !PT_ANY_UNSORTED) {
+            cswap(t0, c0, t1, c1);
+            cswap(t2, c2, t3, c3);
+            cswap(t0, c0, t2, c2);
+            cswap(t1, c1, t3, c3);
+            cswap(t1, c1, t2, c2);
+        }
+        if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
+        {
+            int sp = s.sp;
+            stk[sp * stride] = c3;
+            sp += c3 != kEmptyChild;
+            stk[sp * stride] = c2;
+            sp += c2 != kEmptyChild;
+            stk[sp * stride] = c1;
+            sp += c1 != kEmptyChild;
+            s.sp = sp;
+        }
+        s.cur = c0;
+    }
+    // hand-off: a leaf in the node slot moves to a free leaf slot; refill the node slot
+    if (s.cur == kEmptyChild) stack_pop<DEPTH>(s, stk, stride, spill);
+    if (s.cur < 0 && s.cur != kEmptyChild && s.leaf == kEmptyChild) {
+        s.leaf = s.cur;
+        stack_pop<DEPTH>(s, stk, stride, spill);
+    }
+    return s.cur == kEmptyChild && s.leaf == kEmptyChild;
+#else
+    return trav_step_single<ANY, STATS, DEPTH, TEX>(S, s, stk, stride, spill, ts);
+#endif
 }
 
 // Whole traversal of one ray (megakernel, k_trace).
