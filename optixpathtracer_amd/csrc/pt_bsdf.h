@@ -417,7 +417,15 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
     return mk(b.color.x * c / b.pdf, b.color.y * c / b.pdf, b.color.z * c / b.pdf);
 }
 
-__device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+#ifndef PT_LAYERED_INLINE
+#define PT_LAYERED_INLINE 0
+#endif
+#if PT_LAYERED_INLINE
+#define PT_LAYERED_ATTR __forceinline__
+#else
+#define PT_LAYERED_ATTR __noinline__
+#endif
+__device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
     // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code)
     const int mode = kRadiance;
     const float thickness = 0.01f;
@@ -461,42 +469,42 @@ __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness,
             }
             z = (z == thickness) ? 0.0f : thickness;
             beta = beta * transmittance(thickness, w);
-            if (z == exitZ) {
-                ok = layer_sample(exitTop, seed, albedo, roughness, -w, bs, mode, true, false);
-                if (bs_bad(ok, bs)) break;
-                beta = beta * bs_weight(bs);
-                w = bs.dir;
-            } else {
-                if (!nonExitSpec) {
+            // The reference branches on z == exitZ (GlossyDiffuse.h:315-360); lanes of a wave
+            // disagree on exitZ, so both branches would run every depth.  Here the two
+            // layer_sample calls are one call on the selected layer, with the NEE terms of the
+            // non-exit branch predicated around it: the same operations and random numbers.
+            // (Flattening the sample and depth loops into one loop of steps, so lanes start
+            // their next sample early, was 40 % slower: DESIGN.md §5.)
+            const bool atExit = z == exitZ;
+            if (!atExit && !nonExitSpec) {
+                float wt = 1.0f;
+                if (!exitSpec)
+                    wt = power_heuristic(wis.pdf, layer_pdf(nonExitTop, roughness, -w, -wis.dir, true, true));
+                f3 lf = layer_f(nonExitTop, albedo, roughness, -w, -wis.dir, mode);
+                float ac = abs_cos_theta(wis.dir);
+                float tr = transmittance(thickness, wis.dir);
+                f3 t1 = beta * lf;
+                t1 = t1 * ac;
+                t1 = t1 * wt;
+                t1 = t1 * tr;
+                t1 = t1 * wis.color;
+                t1 = t1 / wis.pdf;
+                f = f + t1;
+            }
+            ok = layer_sample(atExit ? exitTop : nonExitTop, seed, albedo, roughness, -w, bs, mode, true, false);
+            if (bs_bad(ok, bs)) break;
+            beta = beta * bs_weight(bs);
+            w = bs.dir;
+            if (!atExit && !exitSpec) {
+                f3 fExit = layer_f(exitTop, albedo, roughness, -w, wi, mode);
+                if (!is_zero(fExit)) {
                     float wt = 1.0f;
-                    if (!exitSpec)
-                        wt = power_heuristic(wis.pdf, layer_pdf(nonExitTop, roughness, -w, -wis.dir, true, true));
-                    f3 lf = layer_f(nonExitTop, albedo, roughness, -w, -wis.dir, mode);
-                    float ac = abs_cos_theta(wis.dir);
-                    float tr = transmittance(thickness, wis.dir);
-                    f3 t1 = beta * lf;
-                    t1 = t1 * ac;
+                    if (!nonExitSpec) wt = power_heuristic(bs.pdf, layer_pdf(exitTop, roughness, -w, wi, false, true));
+                    float tr = transmittance(thickness, bs.dir);
+                    f3 t1 = beta * tr;
+                    t1 = t1 * fExit;
                     t1 = t1 * wt;
-                    t1 = t1 * tr;
-                    t1 = t1 * wis.color;
-                    t1 = t1 / wis.pdf;
                     f = f + t1;
-                }
-                ok = layer_sample(nonExitTop, seed, albedo, roughness, -w, bs, mode, true, false);
-                if (bs_bad(ok, bs)) break;
-                beta = beta * bs_weight(bs);
-                w = bs.dir;
-                if (!exitSpec) {
-                    f3 fExit = layer_f(exitTop, albedo, roughness, -w, wi, mode);
-                    if (!is_zero(fExit)) {
-                        float wt = 1.0f;
-                        if (!nonExitSpec) wt = power_heuristic(bs.pdf, layer_pdf(exitTop, roughness, -w, wi, false, true));
-                        float tr = transmittance(thickness, bs.dir);
-                        f3 t1 = beta * tr;
-                        t1 = t1 * fExit;
-                        t1 = t1 * wt;
-                        f = f + t1;
-                    }
                 }
             }
         }
@@ -504,7 +512,7 @@ __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness,
     return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
 }
 
-__device__ __noinline__ bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+__device__ PT_LAYERED_ATTR bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
     // GlossyDiffuse.h:372-524
     const int mode = kRadiance;
     const float thickness = 0.01f;

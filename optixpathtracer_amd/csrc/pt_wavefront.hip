@@ -72,10 +72,17 @@ inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * k
 // starves waves.)
 constexpr int kBlockSh = 1024;
 constexpr int kWavesSh = kBlockSh / 64;
+// k_shade_b (Default / Layered: the stochastic GlossyDiffuse eval + sample) needs more than
+// the 128 VGPRs a 1024-thread block allows, so it runs in smaller blocks.
+#ifndef PT_SHB_BLOCK
+#define PT_SHB_BLOCK 1024
+#endif
+constexpr int kBlockShB = PT_SHB_BLOCK;
 
 // Block-wide compaction: every thread of the block calls this (uniform control flow);
 // threads with pred get consecutive slots.  `lds` is kWavesSh + 1 ints of shared memory
 // private to this call site.
+template <int WAVES = kWavesSh>
 __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     const unsigned long long m = __ballot(pred ? 1 : 0);
     const int prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -84,15 +91,15 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     __syncthreads();
     if (threadIdx.x == 0) {
         int tot = 0;
-        for (int w = 0; w < kWavesSh; ++w) {
+        for (int w = 0; w < WAVES; ++w) {
             const int c = lds[w];
             lds[w] = tot;
             tot += c;
         }
-        lds[kWavesSh] = tot > 0 ? atomicAdd(counter, tot) : 0;
+        lds[WAVES] = tot > 0 ? atomicAdd(counter, tot) : 0;
     }
     __syncthreads();
-    return lds[kWavesSh] + lds[wave] + prefix;
+    return lds[WAVES] + lds[wave] + prefix;
 }
 
 // Paths of nf consecutive frames are in flight together (path q = f * P + pixel), so every
@@ -426,16 +433,16 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S
 }
 
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockSh) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
-    __shared__ int lds_q[kWavesSh + 1];
-    if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
+    __shared__ int lds_q[kBlockShB / 64 + 1];
+    if ((int)(blockIdx.x * kBlockShB) >= n) return;  // block-uniform
     {
-        const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+        const int i = (int)(blockIdx.x * kBlockShB + threadIdx.x);
         const bool valid = i < n;
         bool emit_next = false;
         f3 o, d;
@@ -477,7 +484,7 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_b(DevScene S, DevLaunch L, W
                 }
             }
         }
-        const int qi = block_append(cnt(W, b + 1, kQueue), emit_next, lds_q);
+        const int qi = block_append<kBlockShB / 64>(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
             nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -535,7 +542,8 @@ hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, con
     } else if (phase == 0) {
         hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b);
     } else {
-        hipLaunchKernelGGL((k_shade_b<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b);
+        hipLaunchKernelGGL((k_shade_b<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L, W,
+                           b);
     }
     return hipGetLastError();
 }
