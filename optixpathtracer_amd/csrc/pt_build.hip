@@ -259,6 +259,181 @@ __global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, 
 }
 
 
+// ---- SAH-optimal BVH4 collapse (default; PT_SAH_COLLAPSE=0 restores the greedy one) --------
+// Bottom-up dynamic programme over the binary tree (the wide-BVH collapse of Ylitie, Karras &
+// Laine 2017, "Efficient Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs",
+// for 4-wide nodes): cost[n][j] = cheapest SAH cost of covering subtree n with at most j
+// BVH4 children, each one a BVH4 node or a leaf of <= kSahLeafMax consecutive triangles:
+//   single(n)  = min(A(n) * cTri * count(n)            [leaf, count <= kSahLeafMax],
+//                   A(n) * cNode + min_a cost[L][a] + cost[R][4 - a])   [BVH4 node]
+//   cost[n][1] = single(n);  cost[n][j] = min(single(n), min_a cost[L][a] + cost[R][j - a])
+// The top-down k_collapse_sah then replays the recorded choices.  With the dual traversal
+// step (pt_device.h) a triangle test overlaps a node visit, hence cTri < cNode.
+#ifndef PT_SAH_COLLAPSE
+#define PT_SAH_COLLAPSE 1
+#endif
+#ifndef PT_SAH_LEAF_MAX
+#define PT_SAH_LEAF_MAX 4
+#endif
+#ifndef PT_SAH_CTRI
+#define PT_SAH_CTRI 0.5f
+#endif
+constexpr int kSahLeafMax = PT_SAH_LEAF_MAX;
+static_assert(kSahLeafMax >= 1 && kSahLeafMax <= 8, "leaf count is encoded in 3 bits");
+constexpr float kSahCNode = 1.0f;
+constexpr float kSahCTri = PT_SAH_CTRI;
+
+// Decision word of an internal node: bits 2(j-2)..2(j-2)+1 for j = 2..4 = left pieces a of the
+// best split into j (0 = keep single); bits 6..7 = left pieces of the node's own 4-way split;
+// bit 8 = single is a leaf.
+__device__ __forceinline__ int dp_split(int dec, int j) { return (dec >> (2 * (j - 2))) & 3; }
+__device__ __forceinline__ int dp_node_split(int dec) { return (dec >> 6) & 3; }
+__device__ __forceinline__ bool dp_is_leaf(int dec) { return (dec >> 8) & 1; }
+
+__global__ void k_parents(const int2* bchild, int nb, int* parent, int* leafparent) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nb) return;
+    const int2 c = bchild[i];
+    if (c.x >= 0) parent[c.x] = i; else leafparent[~c.x] = i;
+    if (c.y >= 0) parent[c.y] = i; else leafparent[~c.y] = i;
+}
+
+__device__ __forceinline__ float4 dp_load(const float4* p) {
+    const float* f = reinterpret_cast<const float*>(p);
+    return make_float4(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __hip_atomic_load(f + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __hip_atomic_load(f + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __hip_atomic_load(f + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// One thread per triangle walks up; the second child to finish computes the parent (the
+// usual bottom-up refit hand-off through a per-node arrival counter).
+__global__ void k_sah_dp(BinTree B, int n, const int* parent, const int* leafparent, int* visits, float4* dpc,
+                         int* dpd) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int node = leafparent[t];
+    while (node >= 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (atomicAdd(&visits[node], 1) == 0) return;  // the sibling subtree is not done yet
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const int2 ch = B.child[node];
+        float cl[5], cr[5];
+        const int kids[2] = {ch.x, ch.y};
+        for (int k = 0; k < 2; ++k) {
+            float* c = k == 0 ? cl : cr;
+            const int code = kids[k];
+            if (code < 0) {  // one triangle: always a leaf
+                float4 lo = B.leafbox[2 * ~code], hi = B.leafbox[2 * ~code + 1];
+                float v = half_area(lo, hi) * kSahCTri;
+                c[1] = c[2] = c[3] = c[4] = v;
+            } else {
+                float4 v = dp_load(dpc + code);
+                c[1] = v.x; c[2] = v.y; c[3] = v.z; c[4] = v.w;
+            }
+        }
+        const float area = half_area(B.box[2 * node], B.box[2 * node + 1]);
+        const int2 r = B.range[node];
+        const int count = r.y - r.x + 1;
+        const float inf = __int_as_float(0x7f800000);
+        float best4 = inf;
+        int a4 = 1;
+        for (int a = 1; a <= 3; ++a) {
+            const float v = cl[a] + cr[4 - a];
+            if (v < best4) { best4 = v; a4 = a; }
+        }
+        const float node_cost = area * kSahCNode + best4;
+        const float leaf_cost = count <= kSahLeafMax ? area * kSahCTri * (float)count : inf;
+        const bool leaf = leaf_cost <= node_cost;
+        const float single = leaf ? leaf_cost : node_cost;
+        float out[5];
+        int dec = (a4 << 6) | (leaf ? 256 : 0);
+        out[1] = single;
+        for (int j = 2; j <= 4; ++j) {
+            float bj = single;
+            int aj = 0;
+            for (int a = 1; a < j; ++a) {
+                const float v = cl[a] + cr[j - a];
+                if (v < bj) { bj = v; aj = a; }
+            }
+            out[j] = bj;
+            dec |= aj << (2 * (j - 2));
+        }
+        dpc[node] = make_float4(out[1], out[2], out[3], out[4]);
+        dpd[node] = dec;
+        node = parent[node];
+    }
+}
+
+// One BVH4 node per work item (binary code, BVH4 slot): children from the DP choices.
+__global__ void k_collapse_sah(BinTree B, const int* dpd, const int2* work, int nwork, BNode4* out, int* counter,
+                               int2* next, int* nnext) {
+    int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwork) return;
+    const int2 item = work[w];
+    int c[4];
+    int n = 0;
+    if (item.x >= 0) {
+        int st_code[8], st_j[8], sp = 0;
+        const int2 ch = B.child[item.x];
+        const int a = dp_node_split(dpd[item.x]);
+        st_code[sp] = ch.y; st_j[sp++] = 4 - a;
+        st_code[sp] = ch.x; st_j[sp++] = a;
+        while (sp > 0) {
+            --sp;
+            const int x = st_code[sp], j = st_j[sp];
+            const int s = (x < 0 || j < 2) ? 0 : dp_split(dpd[x], j);
+            if (s == 0) {
+                c[n++] = x;
+            } else {
+                const int2 xc = B.child[x];
+                st_code[sp] = xc.y; st_j[sp++] = j - s;
+                st_code[sp] = xc.x; st_j[sp++] = s;
+            }
+        }
+    } else {  // degenerate scene: the root is a single leaf
+        c[n++] = item.x;
+    }
+    float lo[3][4], hi[3][4];
+    int cc[4];
+    for (int k = 0; k < 4; ++k) {
+        if (k >= n) {
+            cc[k] = kEmptyChild;
+            for (int a = 0; a < 3; ++a) {  // inverted box: never hit (see k_collapse)
+                lo[a][k] = __int_as_float(0x7f800000);
+                hi[a][k] = -__int_as_float(0x7f800000);
+            }
+            continue;
+        }
+        float4 l4, h4;
+        code_box(B, c[k], l4, h4);
+        float l[3] = {l4.x, l4.y, l4.z}, h[3] = {h4.x, h4.y, h4.z};
+        for (int a = 0; a < 3; ++a) {
+            lo[a][k] = l[a] - pad_amount(l[a]);
+            hi[a][k] = h[a] + pad_amount(h[a]);
+        }
+        const bool leaf = c[k] < 0 || dp_is_leaf(dpd[c[k]]);
+        if (leaf) {
+            cc[k] = ~((code_first(B, c[k]) << 3) | (code_count(B, c[k]) - 1));
+        } else {
+            int slot = atomicAdd(counter, 1);
+            cc[k] = slot;
+            int q = atomicAdd(nnext, 1);
+            next[q] = make_int2(c[k], slot);
+        }
+    }
+    BNode4 nd;
+    nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    nd.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    nd.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    nd.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    nd.child = make_int4(cc[0], cc[1], cc[2], cc[3]);
+    nd.pad = make_int4(0, 0, 0, 0);
+    out[item.y] = nd;
+}
+
 // ---- PLOC ---------------------------------------------------------------------------------
 #ifndef PT_PLOC_RADIUS
 #define PT_PLOC_RADIUS 8
@@ -496,6 +671,8 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     float4 *st = nullptr, *bbox = nullptr;
     int2 *bchild = nullptr, *brange = nullptr, *work = nullptr, *work2 = nullptr;
     int* cnt = nullptr;  // [0] node counter, [1] next-level work count
+    int *dp_parent = nullptr, *dp_leafparent = nullptr, *dp_visits = nullptr, *dp_dec = nullptr;
+    float4* dp_cost = nullptr;
     void* temp = nullptr;
     size_t temp_bytes = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -567,14 +744,33 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             B.leafbox = st;
             root = n > 1 ? 0 : ~0;
         }
+        if (PT_SAH_COLLAPSE && root >= 0) {  // SAH DP over the binary tree (n >= 2)
+            PT_TRY(hipMalloc(&dp_parent, sizeof(int) * nbin));
+            PT_TRY(hipMalloc(&dp_leafparent, sizeof(int) * n));
+            PT_TRY(hipMalloc(&dp_visits, sizeof(int) * nbin));
+            PT_TRY(hipMalloc(&dp_cost, sizeof(float4) * nbin));
+            PT_TRY(hipMalloc(&dp_dec, sizeof(int) * nbin));
+            PT_TRY(hipMemsetAsync(dp_visits, 0, sizeof(int) * nbin, stream));
+            PT_TRY(hipMemsetAsync(dp_parent, 0xff, sizeof(int) * nbin, stream));  // root: -1
+            hipLaunchKernelGGL(k_parents, dim3(grid_for(nbin, 256)), dim3(256), 0, stream, B.child, nbin, dp_parent,
+                               dp_leafparent);
+            PT_TRY(hipGetLastError());
+            hipLaunchKernelGGL(k_sah_dp, dim3(grid_for(n, 256)), dim3(256), 0, stream, B, n, dp_parent, dp_leafparent,
+                               dp_visits, dp_cost, dp_dec);
+            PT_TRY(hipGetLastError());
+        }
         // root work item: binary root (or the single leaf ~0) -> BVH4 slot 0
         int2 rw = make_int2(root, 0);
         PT_TRY(hipMemcpyAsync(work, &rw, sizeof(int2), hipMemcpyHostToDevice, stream));
         PT_TRY(hipMemcpyAsync(cnt, h_cnt, sizeof(int) * 2, hipMemcpyHostToDevice, stream));
         while (nwork > 0) {
             PT_TRY(hipMemsetAsync(cnt + 1, 0, sizeof(int), stream));
-            hipLaunchKernelGGL(k_collapse, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, work, nwork,
-                               out.nodes, cnt, work2, cnt + 1);
+            if (dp_dec)
+                hipLaunchKernelGGL(k_collapse_sah, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, dp_dec, work,
+                                   nwork, out.nodes, cnt, work2, cnt + 1);
+            else
+                hipLaunchKernelGGL(k_collapse, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, work, nwork,
+                                   out.nodes, cnt, work2, cnt + 1);
             PT_TRY(hipGetLastError());
             PT_TRY(hipMemcpyAsync(h_cnt, cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
             PT_TRY(hipStreamSynchronize(stream));
@@ -593,7 +789,8 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
 done:
     (void)hipStreamSynchronize(stream);
     for (void* p : {(void*)keys, (void*)vals, (void*)keys2, (void*)vals2, (void*)st, (void*)bchild, (void*)brange,
-                    (void*)bbox, (void*)work, (void*)work2, (void*)cnt, temp})
+                    (void*)bbox, (void*)work, (void*)work2, (void*)cnt, temp, (void*)dp_parent,
+                    (void*)dp_leafparent, (void*)dp_visits, (void*)dp_cost, (void*)dp_dec})
         if (p) (void)hipFree(p);
     for (void* p : owned) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
