@@ -516,11 +516,13 @@ __device__ __forceinline__ void stack_pop(TravState& s, int* __restrict__ stk, i
 // work in both, so a ray finishes in ~max(nodes, triangles) steps instead of their sum.
 // Leaves are therefore tested out of front-to-back order, which the (t, index) closest-hit
 // rule makes harmless; culling stays conservative (best only shrinks).
+// `tri_ok` (wave-uniform) lets the caller postpone the triangle half of the step until enough
+// lanes hold a leaf (trace_slice); lanes keep traversing nodes meanwhile.
 template <int ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
-                                          int* spill, TravStats& ts) {
+                                          int* spill, TravStats& ts, bool tri_ok = true) {
 #if PT_DUAL_STEP
-    if (s.leaf != kEmptyChild) {
+    if (tri_ok && s.leaf != kEmptyChild) {
         if (leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
     }
     if (s.cur >= 0) {

@@ -127,6 +127,9 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
 #define PT_REFILL_MIN 8
 #endif
 constexpr int kRefillMin = PT_REFILL_MIN;
+#ifndef PT_TRI_BATCH
+#define PT_TRI_BATCH 16  // lanes with a pending leaf before a wave runs its triangle tests
+#endif
 
 __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -162,8 +165,19 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
             }
         }
         next = min(next + __popcll(m), end);
-        if (!__any(ri >= 0 ? 1 : 0)) break;
-        if (ri >= 0 && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts)) {
+        const unsigned long long act = __ballot(ri >= 0 ? 1 : 0);
+        if (!act) break;
+#if PT_DUAL_STEP && PT_TRI_BATCH > 0
+        // postponed leaves: run the triangle half of the step once enough lanes hold a leaf,
+        // or when too few lanes have a node left to visit (then the leaves are the work)
+        const int n_act = __popcll(act);
+        const int n_leaf = __popcll(__ballot(ri >= 0 && st.leaf != kEmptyChild ? 1 : 0));
+        const int n_node = __popcll(__ballot(ri >= 0 && st.cur >= 0 ? 1 : 0));
+        const bool tri_ok = n_leaf >= min(PT_TRI_BATCH, n_act) || 2 * n_node < n_act;
+#else
+        const bool tri_ok = true;
+#endif
+        if (ri >= 0 && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts, tri_ok)) {
             finish(ri, st);
             ri = -1;
         }
