@@ -78,6 +78,9 @@ constexpr int kWavesSh = kBlockSh / 64;
 #define PT_SHB_BLOCK 1024
 #endif
 constexpr int kBlockShB = PT_SHB_BLOCK;
+#ifndef PT_SHB_BUCKET
+#define PT_SHB_BUCKET 1  // k_shade_b groups its compacted items by material (conductor coin)
+#endif
 
 // Block-wide compaction: every thread of the block calls this (uniform control flow);
 // threads with pred get consecutive slots.  `lds` is kWavesSh + 1 ints of shared memory
@@ -446,63 +449,123 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S
         [&](int j, const TravState& st) { W.vis[__float_as_int(W.sh_o[j].w)] = st.h.tri >= 0 ? 0 : 1; });
 }
 
+// Block-local stable two-bucket compaction: threads with `pred` get consecutive slots, those
+// with bucket 0 first; returns the slot (valid if pred) and the block's total.
+template <int WAVES>
+__device__ __forceinline__ int block_bucket_scan(bool pred, bool bucket1, int* lds, int& total) {
+    const unsigned long long m0 = __ballot(pred && !bucket1 ? 1 : 0);
+    const unsigned long long m1 = __ballot(pred && bucket1 ? 1 : 0);
+    const int wave = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        lds[wave] = __popcll(m0);
+        lds[WAVES + wave] = __popcll(m1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < 2 * WAVES; ++w) {  // bucket 0 of every wave, then bucket 1
+            const int c = lds[w];
+            lds[w] = tot;
+            tot += c;
+        }
+        lds[2 * WAVES] = tot;
+    }
+    __syncthreads();
+    total = lds[2 * WAVES];
+    const unsigned long long m = bucket1 ? m1 : m0;
+    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    return lds[(bucket1 ? WAVES : 0) + wave] + pre;
+}
+
+// Second half of a Default / Layered bounce.  The stochastic GlossyDiffuse eval and sample
+// dominate (≈10^4 instructions per call) and a wave pays for its slowest lane,
+// so the block first compacts its items in LDS: the NEE eval runs on the items whose light is
+// visible, packed into the block's first waves and grouped by material (conductor coin), then
+// the BSDF sample runs on the items that hit a surface, packed and grouped the same way.
+// Every path still sees the same operations and random numbers in the same order (the NEE
+// eval updates the path seed in W.beta before the sample reads it); only which thread works
+// on which path, and the order of the appends to the next queue, change.
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
+    constexpr int kW = kBlockShB / 64;
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
-    __shared__ int lds_q[kBlockShB / 64 + 1];
+    __shared__ int lds_q[kW + 1];
+    __shared__ int lds_scan_a[2 * kW + 1], lds_scan_b[2 * kW + 1];  // separate: no reuse race
+    __shared__ int lds_nee[kBlockShB], lds_smp[kBlockShB];
     if ((int)(blockIdx.x * kBlockShB) >= n) return;  // block-uniform
-    {
-        const int i = (int)(blockIdx.x * kBlockShB + threadIdx.x);
-        const bool valid = i < n;
-        bool emit_next = false;
-        f3 o, d;
-        int path = 0;
-        if (valid) {
-            const float4 a = ro[i], c = rd[i];
-            path = __float_as_int(a.w);
-            const Hit h = decode_hit(W.hit[i]);
-            if (h.tri >= 0) {
-                d = mk(c.x, c.y, c.z);
-                SurfaceHit sf;
-                reconstruct<TEX>(S, h, d, sf);
-                float4 bv = W.beta[path];
-                uint32_t seed = __float_as_uint(bv.w);
-                f3 beta = mk(bv.x, bv.y, bv.z);
-                const int aux = W.aux[path];
-                const bool conductor = aux & 1;
-                const int li = aux >> 1;
-                if (L.n_lights > 0 && W.vis[path]) {
-                    const float P = L.n_lights == 1 ? 1.0f : 1.0f / (float)L.n_lights;
-                    const DevLight lt = L.lights[li];
-                    f3 lpos = mk(lt.px, lt.py, lt.pz);
-                    f3 lds = to_local(sf.fr, normalize(lpos - sf.pos));
-                    f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);
-                    f3 spectrum = f * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
-                    if (!is_zero(spectrum)) {
-                        f3 dd = sf.pos - lpos;
-                        float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
-                        f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
-                        f3 add = ((beta * spectrum) * Li) / (P * 1.0f);
-                        float4 l = W.L[path];
-                        W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
-                    }
-                }
-                BSample bs;
-                if (bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
-                    emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
-                    W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
-                }
-            }
+    const int i = (int)(blockIdx.x * kBlockShB + threadIdx.x);
+    bool hit = false, nee = false, conductor = false;
+    if (i < n) {
+        const int path = __float_as_int(ro[i].w);
+        hit = __float_as_int(W.hit[i].w) != kMissTri;
+        if (hit) {
+            conductor = PT_SHB_BUCKET && (W.aux[path] & 1);
+            nee = L.n_lights > 0 && W.vis[path];
         }
-        const int qi = block_append<kBlockShB / 64>(cnt(W, b + 1, kQueue), emit_next, lds_q);
-        if (emit_next) {
-            no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
-            nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
+    }
+    int n_nee, n_smp;
+    const int s_nee = block_bucket_scan<kW>(nee, conductor, lds_scan_a, n_nee);
+    if (nee) lds_nee[s_nee] = i;
+    const int s_smp = block_bucket_scan<kW>(hit, conductor, lds_scan_b, n_smp);
+    if (hit) lds_smp[s_smp] = i;
+    __syncthreads();
+    if ((int)threadIdx.x < n_nee) {  // NEE: the light is visible (devicePrograms.cu:446-472)
+        const int j = lds_nee[threadIdx.x];
+        const float4 a = ro[j], c = rd[j];
+        const int path = __float_as_int(a.w);
+        const Hit h = decode_hit(W.hit[j]);
+        SurfaceHit sf;
+        reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
+        const float4 bv = W.beta[path];
+        uint32_t seed = __float_as_uint(bv.w);
+        const f3 beta = mk(bv.x, bv.y, bv.z);
+        const int aux = W.aux[path];
+        const int li = aux >> 1;
+        const float P = L.n_lights == 1 ? 1.0f : 1.0f / (float)L.n_lights;
+        const DevLight lt = L.lights[li];
+        f3 lpos = mk(lt.px, lt.py, lt.pz);
+        f3 lds = to_local(sf.fr, normalize(lpos - sf.pos));
+        f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
+        f3 spectrum = f * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+        if (!is_zero(spectrum)) {
+            f3 dd = sf.pos - lpos;
+            float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+            f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+            f3 add = ((beta * spectrum) * Li) / (P * 1.0f);
+            float4 l = W.L[path];
+            W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
         }
+        W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));  // f may draw
+    }
+    __syncthreads();  // the sample below reads the seeds written above (same block)
+    bool emit_next = false;
+    f3 o, d;
+    int path = 0;
+    if ((int)threadIdx.x < n_smp) {  // BSDF sample + continuation (devicePrograms.cu:474-509)
+        const int j = lds_smp[threadIdx.x];
+        const float4 a = ro[j], c = rd[j];
+        path = __float_as_int(a.w);
+        const Hit h = decode_hit(W.hit[j]);
+        d = mk(c.x, c.y, c.z);
+        SurfaceHit sf;
+        reconstruct<TEX>(S, h, d, sf);
+        const float4 bv = W.beta[path];
+        uint32_t seed = __float_as_uint(bv.w);
+        f3 beta = mk(bv.x, bv.y, bv.z);
+        BSample bs;
+        if (bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, W.aux[path] & 1, sf.wo, bs)) {
+            emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
+            W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
+        }
+    }
+    const int qi = block_append<kW>(cnt(W, b + 1, kQueue), emit_next, lds_q);
+    if (emit_next) {
+        no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
+        nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
     }
 }
 
