@@ -142,6 +142,28 @@ __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
     end = min(n, first + per);
 }
 
+// Queue records are streamed once per launch; PT_NT_QUEUE marks those loads and stores
+// non-temporal so they do not evict BVH / triangle lines from L2.
+#ifndef PT_NT_QUEUE
+#define PT_NT_QUEUE 0
+#endif
+typedef float pt_v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldq(const float4* p) {
+#if PT_NT_QUEUE
+    const pt_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pt_v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stq(float4* p, float4 v) {
+#if PT_NT_QUEUE
+    __builtin_nontemporal_store(pt_v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<pt_v4f*>(p));
+#else
+    *p = v;
+#endif
+}
+
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
@@ -198,14 +220,14 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
     trace_slice<kRayClosest, STATS, TEX>(
         S, n, stk, ts,
         [&](int ri, TravState& st) {
-            const float4 a = ro[ri], c = rd[ri];
+            const float4 a = ldq(ro + ri), c = ldq(rd + ri);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
         },
         [&](int ri, const TravState& st) {
             const Hit& h = st.h;
-            W.hit[ri] = h.tri >= 0
-                            ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                            : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+            stq(W.hit + ri, h.tri >= 0 ? make_float4(h.t, h.u, h.v,
+                                                     __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                                       : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri)));
         });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n);  // path segments
@@ -346,11 +368,11 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
         S, n_ext + n_sh, stk, ts,
         [&](int i, TravState& st) {
             if (i < n_ext) {
-                const float4 a = ro[i], c = rd[i];
+                const float4 a = ldq(ro + i), c = ldq(rd + i);
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
             } else {
                 const int j = i - n_ext;
-                const float4 a = W.sh_o[j], c = W.sh_d[j];
+                const float4 a = ldq(W.sh_o + j), c = ldq(W.sh_d + j);
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
                 st.any = true;
             }
@@ -358,13 +380,13 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
         [&](int i, const TravState& st) {
             const Hit& h = st.h;
             if (i < n_ext) {
-                W.hit[i] = h.tri >= 0
-                               ? make_float4(h.t, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                               : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+                stq(W.hit + i, h.tri >= 0 ? make_float4(h.t, h.u, h.v,
+                                                        __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                                          : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri)));
             } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
                 const int j = i - n_ext;
                 const int path = __float_as_int(W.sh_o[j].w);
-                const float4 k = W.sh_c[j];
+                const float4 k = ldq(W.sh_c + j);
                 const float4 l = W.L[path];
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
