@@ -58,6 +58,22 @@ def random_rays(scene, n, seed=0, tmax=100.0):
     tgt = np.einsum("ij,ijk->ik", w, tris[ti])
     d[:k] = tgt - o[:k]
     d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    # axis-aligned rays (the other components +0 or -0) aimed at triangle points from outside:
+    # exercise the slab test's zero-direction handling and the near/far plane selection
+    k2 = n // 6
+    if k2 > 0:
+        ti = rng.integers(0, len(tris), size=k2)
+        w = rng.dirichlet([1.0, 1.0, 1.0], size=k2)
+        w[: k2 // 2] = np.eye(3)[rng.integers(0, 3, size=k2 // 2)]
+        tgt = np.einsum("ij,ijk->ik", w, tris[ti]).astype(np.float32)
+        axis = rng.integers(0, 3, size=k2)
+        sign = rng.choice([-1.0, 1.0], size=k2)
+        dd = np.where(rng.random((k2, 3)) < 0.5, np.float32(-0.0), np.float32(0.0)).astype(np.float32)
+        dd[np.arange(k2), axis] = sign
+        oo = tgt.copy()
+        oo[np.arange(k2), axis] -= (sign * rng.uniform(0.5, 3.0, size=k2)).astype(np.float32)
+        o[k: k + k2] = oo
+        d[k: k + k2] = dd
     rays = np.zeros((n, 8), np.float32)
     rays[:, 0:3] = o
     rays[:, 3:6] = d
