@@ -145,6 +145,12 @@ class OptixRendererT {
     void DownloadMean(Vec3 h_pixels[], uint32_t spp) {
         check(pt_accum_download(r_, reinterpret_cast<float*>(h_pixels), 1.0f / (float)spp), "pt_accum_download");
     }
+    // Whole image in one call: spp frames from first_frame_id, mean to h_pixels (W*H vec3).
+    template <class Vec3>
+    void RenderAccumulate(uint32_t spp, uint32_t first_frame_id, Vec3 h_pixels[]) {
+        check(pt_render_accumulate(r_, spp, first_frame_id, reinterpret_cast<float*>(h_pixels)),
+              "pt_render_accumulate");
+    }
     pt_renderer* handle() { return r_; }
 
    private:

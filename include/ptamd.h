@@ -153,6 +153,11 @@ int pt_render(pt_renderer* r, float* host_rgb);
  * order, into the fp32 sum buffer.  Asynchronous on the library stream. */
 int pt_accum_clear(pt_renderer* r);
 int pt_render_frames(pt_renderer* r, uint32_t first_frame_id, uint32_t n_frames);
+/* One call for a whole image (SURVEY §8(b) "pt_render_accumulate"): clear, render frame ids
+ * first_frame_id .. first_frame_id+spp-1 into the sum buffer, then (if host_rgb_mean is not
+ * NULL) download the mean, sum / spp, as the reference's running-mean display converges to
+ * (OptixView.cpp:232-245 with maxSamples < 0).  Synchronous; the sum stays on the device. */
+int pt_render_accumulate(pt_renderer* r, uint32_t spp, uint32_t first_frame_id, float* host_rgb_mean);
 /* Use caller-owned device memory (W*H*3 floats) as the sum buffer (e.g. an RCCL buffer);
  * NULL reverts to the internal buffer. */
 int pt_set_accum_device_buffer(pt_renderer* r, float* device_sum_rgb);

@@ -123,6 +123,7 @@ SIGNATURES = {
     "pt_render": (C.c_int, [_R, _FP]),
     "pt_accum_clear": (C.c_int, [_R]),
     "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),
+    "pt_render_accumulate": (C.c_int, [_R, C.c_uint32, C.c_uint32, _FP]),
     "pt_set_accum_device_buffer": (C.c_int, [_R, C.c_void_p]),
     "pt_accum_device_ptr": (C.c_void_p, [_R]),
     "pt_accum_download": (C.c_int, [_R, _FP, C.c_float]),

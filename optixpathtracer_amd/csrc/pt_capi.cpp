@@ -632,6 +632,18 @@ int pt_render_frames(pt_renderer* r, uint32_t first_frame_id, uint32_t n_frames)
     return launch_frames(r, r->accum(), first_frame_id, n_frames);
 }
 
+int pt_render_accumulate(pt_renderer* r, uint32_t spp, uint32_t first_frame_id, float* host_rgb_mean) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_render_accumulate: NULL");
+    if (r->width == 0) return fail(PT_ERR_STATE, "pt_render_accumulate: call pt_resize first");
+    if (spp == 0) return fail(PT_ERR_INVALID, "pt_render_accumulate: spp must be > 0");
+    int rc = pt_accum_clear(r);
+    if (rc) return rc;
+    rc = pt_render_frames(r, first_frame_id, spp);
+    if (rc) return rc;
+    if (host_rgb_mean) return pt_accum_download(r, host_rgb_mean, 1.0f / (float)spp);
+    return pt_synchronize(r);
+}
+
 int pt_set_accum_device_buffer(pt_renderer* r, float* device_sum_rgb) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_accum_device_buffer: NULL");
     r->user_accum = device_sum_rgb;

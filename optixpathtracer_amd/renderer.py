@@ -174,6 +174,15 @@ class OptixRenderer:
     def render_frames(self, first_frame_id: int, n_frames: int) -> None:
         check(self.lib.pt_render_frames(self.h, int(first_frame_id), int(n_frames)), "pt_render_frames")
 
+    def render_accumulate(self, spp: int, first_frame_id: int = 1) -> np.ndarray:
+        """Clear, render frame ids first_frame_id .. +spp-1 and return the mean image
+        (pt_render_accumulate); the sum stays in the device accumulator."""
+        w, h = self.size
+        out = np.empty((h, w, 3), np.float32)
+        check(self.lib.pt_render_accumulate(self.h, int(spp), int(first_frame_id), fptr(out)),
+              "pt_render_accumulate")
+        return out
+
     def set_accum_device_buffer(self, ptr: int | None) -> None:
         check(self.lib.pt_set_accum_device_buffer(self.h, C.c_void_p(ptr) if ptr else None),
               "pt_set_accum_device_buffer")

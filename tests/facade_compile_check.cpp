@@ -83,7 +83,12 @@ int main() {
         float mx = 0.0f;
         for (const auto& v : px) mx = v.x > mx ? v.x : mx;
         std::printf("rendered max=%g\n", mx);
-        return mx > 0.0f ? 0 : 3;
+        std::vector<vec3> mean(64);
+        r.RenderAccumulate(4, 1, mean.data());  // extension beyond the reference's six methods
+        float mm = 0.0f;
+        for (const auto& v : mean) mm = v.x > mm ? v.x : mm;
+        std::printf("accumulated max=%g\n", mm);
+        return (mx > 0.0f && mm > 0.0f) ? 0 : 3;
     } catch (const std::exception& e) {
         std::printf("threw: %s\n", e.what());
         return 2;

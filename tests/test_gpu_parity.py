@@ -201,6 +201,10 @@ def test_render_api_semantics(diffuse_scene):
     np.testing.assert_array_equal(r.accum(), one)
     # mean download
     np.testing.assert_allclose(r.accum(scale=1.0 / 11), one / 11, rtol=1e-6)
+    # pt_render_accumulate = clear + render_frames + mean download; the sum stays on the device
+    mean = r.render_accumulate(11, 1)
+    np.testing.assert_array_equal(mean, (one * np.float32(1.0 / 11)).astype(np.float32))
+    np.testing.assert_array_equal(r.accum(), one)
     r.close()
 
 
