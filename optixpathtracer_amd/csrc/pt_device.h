@@ -80,6 +80,9 @@ struct TravStats {
 
 // Reciprocal direction; zero components map to a huge finite value so the fma slab form
 // never produces 0*inf.
+#ifndef PT_CHILD_SORT
+#define PT_CHILD_SORT 2  // 2: full 4-sort of the hit children; 1: nearest first only; 0: none
+#endif
 #ifndef PT_ANY_UNSORTED
 #define PT_ANY_UNSORTED 1
 #endif
@@ -530,12 +533,14 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         float t0, t1, t2, t3;
         int c0, c1, c2, c3;
         node_test(S, s, s.cur, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
-        if (ANY != kRayAny || !PT_ANY_UNSORTED) {
+        if ((ANY != kRayAny || !PT_ANY_UNSORTED) && PT_CHILD_SORT > 0) {
             cswap(t0, c0, t1, c1);
             cswap(t2, c2, t3, c3);
-            cswap(t0, c0, t2, c2);
-            cswap(t1, c1, t3, c3);
-            cswap(t1, c1, t2, c2);
+            cswap(t0, c0, t2, c2);  // c0 nearest
+            if (PT_CHILD_SORT > 1) {
+                cswap(t1, c1, t3, c3);
+                cswap(t1, c1, t2, c2);
+            }
         }
         if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
         {
