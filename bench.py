@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--kernel", type=int, default=2, help="0 = megakernel, 1 = wavefront, 2 = auto")
     ap.add_argument("--frames-per-launch", type=int, default=16)
+    ap.add_argument("--no-dedup-check", action="store_true",
+                    help="skip the extra step timed with pt_set_primary_dedup(0)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
@@ -163,8 +165,28 @@ def main():
         elapsed = float(t.item())
     samples_total = args.width * args.height * args.spp * args.steps * world
     value = samples_total / elapsed / 1e6
+    # Transparency: the same step with every frame's (identical) camera ray traced again
+    # instead of once per pixel per batch (pt_set_primary_dedup; bit-identical images).
+    img = accum.cpu().numpy() if rank == 0 else None  # the timed steps' image
+    value_nodedup = None
+    if args.kernel != 0 and not args.no_dedup_check:
+        r.set_primary_dedup(False)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        step(args.warmup + args.steps)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        e1 = time.perf_counter() - t1
+        if dist is not None:
+            t = torch.tensor([e1], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e1 = float(t.item())
+        value_nodedup = args.width * args.height * args.spp * world / e1 / 1e6
+        r.set_primary_dedup(True)
     if rank == 0:
-        img = accum.cpu().numpy()
         nan_px = int(np.isnan(img).any(axis=-1).sum())
         kernel_s = st["total_render_ms"] / 1e3
         alg_bytes = st["segments"] * BYTES_PER_SEGMENT + st["samples"] * BYTES_PER_SAMPLE
@@ -174,9 +196,10 @@ def main():
             # bracketed by its own HIP event pair on the library stream
             dom = "k_extend+k_trace_pair"
             launches = int(st["trace_kernel_launches"])
-            per_launch_bytes = st["trace_kernel_rays"] * BYTES_PER_TRACE / launches
+            per_launch_bytes = st["trace_kernel_bytes"] / launches
             avg_launch_s = st["trace_kernel_ms"] / 1e3 / launches
-            bytes_def = "48 B per traced ray (ray record read 32 + hit / shadow result write 16)"
+            bytes_def = ("32 B ray record read per traced ray + 16 B per hit / shadow record written "
+                         "(k_extend writes its hit to every frame copy of the batch)")
         else:
             dom = "k_render_mega"
             launches = max(1, int(st["kernel_launches"]))
@@ -220,7 +243,11 @@ def main():
                 "frames_per_launch": args.frames_per_launch,
                 "parallelism": f"spp-shard x{world}",
                 "lbvh_build_ms": round(bvh_ms, 3),
+                "primary_dedup": args.kernel != 0,
             },
+            # one extra step with pt_set_primary_dedup(0): each frame traces its own copy of the
+            # (identical, unjittered) camera rays; same image bit for bit
+            "value_primary_per_frame": None if value_nodedup is None else round(value_nodedup, 3),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),

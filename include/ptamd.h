@@ -111,6 +111,9 @@ typedef struct pt_stats {
     uint64_t trace_kernel_launches;
     uint64_t shadow_rays;        /* NEE shadow rays traced since pt_stats_reset */
     uint64_t trace_kernel_rays;  /* rays traced by the timed trace kernels (k_extend, k_trace_pair) */
+    uint64_t trace_kernel_bytes; /* their algorithmic queue bytes: 32 B per ray read + 16 B per
+                                    hit / shadow record written (k_extend with primary dedup
+                                    writes one record per frame of the batch) */
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -141,6 +144,11 @@ int pt_set_traversal_stats(pt_renderer* r, int32_t enable);
 /* Bracket every wavefront trace launch (k_extend, k_trace_pair) with its own HIP event pair
  * on the library stream (pt_stats.trace_kernel_ms / trace_kernel_launches).  Off by default. */
 int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
+/* Wavefront: the camera ray of a pixel is the same in every frame (no pixel jitter,
+ * devicePrograms.cu:601-623), so a batch of frames traces it once per pixel and copies the
+ * hit record to every frame (default 1).  0 traces every frame's copy; the images are
+ * bit-identical either way. */
+int pt_set_primary_dedup(pt_renderer* r, int32_t enable);
 
 /* OptixRenderer::Render(glm::vec3 h_pixels[]) — OptixRenderer.cpp:617-647: frame.id++,
  * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before

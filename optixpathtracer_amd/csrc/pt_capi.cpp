@@ -125,6 +125,7 @@ struct pt_renderer {
     uint64_t launches = 0;
     // optional per-launch timing of the wavefront's closest-hit trace kernel (k_extend)
     bool kernel_timing = false;
+    bool primary_dedup = true;  // pt_set_primary_dedup
     EventPool tev;
     std::vector<hipEvent_t> tev_frame;  // 2 * max_bounces events handed to one frame
     double trace_ms = 0.0;
@@ -232,7 +233,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
                 tev = r->tev_frame.data();
             }
             PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
-            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, nf, dev_cus,
+            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, nf,
+                                          r->primary_dedup, dev_cus,
                                           r->stream, tev),
                    "wavefront launch");
             PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
@@ -705,6 +707,7 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->trace_kernel_launches = r->trace_launches;
     out->shadow_rays = c[5];
     out->trace_kernel_rays = c[6];
+    out->trace_kernel_bytes = c[7];
     return PT_OK;
 }
 
@@ -842,6 +845,14 @@ int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* pr
 extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_traversal_stats: NULL");
     r->trav_stats = enable != 0;
+    return PT_OK;
+}
+
+extern "C" int pt_set_primary_dedup(pt_renderer* r, int32_t enable) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_primary_dedup: NULL");
+    int rc = collect_pending(r);
+    if (rc) return rc;
+    r->primary_dedup = enable != 0;
     return PT_OK;
 }
 

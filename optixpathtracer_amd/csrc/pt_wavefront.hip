@@ -209,29 +209,38 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
     }
 }
 
+// Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
+// camera rays (one per frame of the batch: the reference has no pixel jitter, so a pixel's ray
+// is identical in every frame, devicePrograms.cu:601-623), so only the first n / dup are traced
+// and each hit record is written to all copies.  The records are bit-identical to tracing every
+// copy; DESIGN.md §5 gives the A/B.
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WFState W, int b, unsigned long long* counters) {
+__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WFState W, int b, int dup,
+                                                                  unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     const int n = *cnt(W, b, kQueue);
+    const int n_trace = n / dup;
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     int* stk = stack + threadIdx.x;
     TravStats ts;
     trace_slice<kRayClosest, STATS, TEX>(
-        S, n, stk, ts,
+        S, n_trace, stk, ts,
         [&](int ri, TravState& st) {
             const float4 a = ldq(ro + ri), c = ldq(rd + ri);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
         },
         [&](int ri, const TravState& st) {
             const Hit& h = st.h;
-            stq(W.hit + ri, h.tri >= 0 ? make_float4(h.t, h.u, h.v,
-                                                     __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                                       : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri)));
+            const float4 rec = h.tri >= 0 ? make_float4(h.t, h.u, h.v,
+                                                        __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                                          : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+            for (int k = 0; k < dup; ++k) stq(W.hit + ri + (size_t)k * n_trace, rec);
         });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
-        atomicAdd(&counters[0], (unsigned long long)n);  // path segments
-        atomicAdd(&counters[6], (unsigned long long)n);  // rays traced by the timed trace kernels
+        atomicAdd(&counters[0], (unsigned long long)n);        // path segments
+        atomicAdd(&counters[6], (unsigned long long)n_trace);  // rays traced by the timed trace kernels
+        atomicAdd(&counters[7], 32ull * (unsigned long long)n_trace + 16ull * (unsigned long long)n);  // bytes
     }
     if (STATS && counters) {
         unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
@@ -395,6 +404,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
         atomicAdd(&counters[6], (unsigned long long)(n_ext + n_sh));  // rays of timed trace kernels
+        atomicAdd(&counters[7], 48ull * (unsigned long long)(n_ext + n_sh));  // their queue bytes
     }
     if (STATS && counters) {
         unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
@@ -707,7 +717,8 @@ void wavefront_free(WFState& W) {
 }
 
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
-                                  uint32_t frame, int nf, int cus, hipStream_t stream, const hipEvent_t* trace_events) {
+                                  uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
+                                  const hipEvent_t* trace_events) {
     const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
@@ -717,22 +728,22 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     const bool fused = fused_mode(mode);
     const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
     int timed = 0;                          // trace launches bracketed by trace_events
-    auto extend = [&](int b) -> hipError_t {
+    auto extend = [&](int b, int dup) -> hipError_t {
         hipError_t r;
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
         if (tex) {
             if (stats)
                 hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockWF),
-                                   0, stream, S, W, b, L.counters);
+                                   0, stream, S, W, b, dup, L.counters);
             else
                 hipLaunchKernelGGL((k_extend<false, true>), occupancy_grid(k_extend<false, true>, cus),
-                                   dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+                                   dim3(kBlockWF), 0, stream, S, W, b, dup, L.counters);
         } else if (stats) {
             hipLaunchKernelGGL((k_extend<true, false>), occupancy_grid(k_extend<true, false>, cus), dim3(kBlockWF), 0,
-                               stream, S, W, b, L.counters);
+                               stream, S, W, b, dup, L.counters);
         } else {
             hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockWF),
-                               0, stream, S, W, b, L.counters);
+                               0, stream, S, W, b, dup, L.counters);
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
         ++timed;
@@ -761,14 +772,14 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     };
     if (fused) {
         // extend(0); then per bounce: shade(b) -> [shadow rays of b + extension rays of b+1]
-        if ((e = extend(0)) != hipSuccess) return e;
+        if ((e = extend(0, primary_dedup ? nf : 1)) != hipSuccess) return e;
         for (int b = 0; b < maxb; ++b) {
             if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
             if ((e = pair(b)) != hipSuccess) return e;
         }
     } else {
         for (int b = 0; b < maxb; ++b) {
-            if ((e = extend(b)) != hipSuccess) return e;
+            if ((e = extend(b, b == 0 && primary_dedup ? nf : 1)) != hipSuccess) return e;
             if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
             if (tex)
                 hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0,

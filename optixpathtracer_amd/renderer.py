@@ -174,6 +174,9 @@ class OptixRenderer:
     def render_frames(self, first_frame_id: int, n_frames: int) -> None:
         check(self.lib.pt_render_frames(self.h, int(first_frame_id), int(n_frames)), "pt_render_frames")
 
+    def set_primary_dedup(self, enable: bool) -> None:
+        check(self.lib.pt_set_primary_dedup(self.h, 1 if enable else 0), "pt_set_primary_dedup")
+
     def render_accumulate(self, spp: int, first_frame_id: int = 1) -> np.ndarray:
         """Clear, render frame ids first_frame_id .. +spp-1 and return the mean image
         (pt_render_accumulate); the sum stays in the device accumulator."""

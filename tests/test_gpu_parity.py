@@ -249,6 +249,17 @@ def test_wavefront_frame_batching_bit_identical(mode):
         assert st["segments"] == sr["segments"]
     mega, _ = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=0)
     np.testing.assert_array_equal(mega, ref)
+    # primary dedup off: every frame traces its own copy of the camera rays
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    r = setup_renderer(sc, 48, 40, 5, kernel=1)
+    r.set_material_mode(mode)
+    r.set_frames_per_launch(4)
+    r.set_primary_dedup(False)
+    r.accum_clear()
+    r.render_frames(7, 11)
+    np.testing.assert_array_equal(r.accum(), ref)
+    r.close()
 
 
 @pytest.mark.parametrize("mode", [1, 0])
