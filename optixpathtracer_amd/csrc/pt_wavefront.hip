@@ -288,8 +288,44 @@ __device__ __forceinline__ bool continue_path(const SurfaceHit& sf, const BSampl
     return next_bounce < max_bounces && length(beta) > 0.00001f;
 }
 
+// Bounce-0 shadow dedup (with primary dedup): a pixel's first hit is the same in every frame
+// of the batch, so its shadow ray toward light li is too.  k_shadow0_setup builds one shadow
+// ray per (pixel, light) from the frame-0 hit, k_shadow_vis traces them into W.vis[pixel *
+// n_lights + light], and the bounce-0 shading reads that table instead of tracing a shadow ray
+// per path.  Same rays, same any-hit answers: the images stay bit-identical.
+__device__ __forceinline__ int vis0_index(const DevLaunch& L, int path, int li) {
+    const int P1 = L.width * L.height;
+    return (path % P1) * L.n_lights + li;  // path = frame * P1 + pixel
+}
+
+template <bool TEX>
+__global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunch L, WFState W) {
+    const int P1 = L.width * L.height;
+    const int nl = L.n_lights;
+    const int n = P1 * nl;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const int p = k / nl, li = k - p * nl;
+        const Hit h = decode_hit(W.hit[p]);  // frame 0's copy (queue 0 is in path order)
+        float4 so = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(k)), sd = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+        if (h.tri >= 0) {  // same arithmetic as the shading kernels' shadow rays
+            const float4 c = W.ray_d[0][p];
+            SurfaceHit sf;
+            reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
+            const DevLight lt = L.lights[li];
+            const f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
+            const f3 o = sf.pos + 1e-3f * sf.ng;
+            const f3 d = normalize(ldir);
+            so = make_float4(o.x, o.y, o.z, __int_as_float(k));
+            sd = make_float4(d.x, d.y, d.z, length(ldir));
+        }
+        W.sh_o[k] = so;
+        W.sh_d[k] = sd;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kShadowQ) = n;
+}
+
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
@@ -332,10 +368,17 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch 
                         float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
                         f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
                         contrib = ((beta * spectrum) * Li) / (P * 1.0f);
-                        so = sf.pos + 1e-3f * sf.ng;
-                        sdir = normalize(ldir);
-                        stmax = length(ldir);
-                        emit_shadow = true;
+                        if (vis0) {  // bounce 0: the (pixel, light) visibility is already known
+                            if (W.vis[vis0_index(L, path, li)]) {
+                                const float4 l = W.L[path];
+                                W.L[path] = make_float4(l.x + contrib.x, l.y + contrib.y, l.z + contrib.z, 0.0f);
+                            }
+                        } else {
+                            so = sf.pos + 1e-3f * sf.ng;
+                            sdir = normalize(ldir);
+                            stmax = length(ldir);
+                            emit_shadow = true;
+                        }
                     }
                 }
                 BSample bs;
@@ -419,7 +462,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
 }
 
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
@@ -446,7 +489,7 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
                 const float P = pick_light(L, seed, li);
                 W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));
                 W.aux[path] = (li << 1) | (conductor ? 1 : 0);
-                if (P > 0.0f) {
+                if (P > 0.0f && !vis0) {
                     const DevLight lt = L.lights[li];
                     f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
                     so = sf.pos + 1e-3f * sf.ng;
@@ -518,7 +561,7 @@ __device__ __forceinline__ int block_bucket_scan(bool pred, bool bucket1, int* l
 // eval updates the path seed in W.beta before the sample reads it); only which thread works
 // on which path, and the order of the appends to the next queue, change.
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     constexpr int kW = kBlockShB / 64;
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
@@ -535,8 +578,9 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
         const int path = __float_as_int(ro[i].w);
         hit = __float_as_int(W.hit[i].w) != kMissTri;
         if (hit) {
-            conductor = PT_SHB_BUCKET && (W.aux[path] & 1);
-            nee = L.n_lights > 0 && W.vis[path];
+            const int aux = W.aux[path];
+            conductor = PT_SHB_BUCKET && (aux & 1);
+            nee = L.n_lights > 0 && W.vis[vis0 ? vis0_index(L, path, aux >> 1) : path];
         }
     }
     int n_nee, n_smp;
@@ -643,36 +687,37 @@ dim3 occupancy_grid(K kernel, int cus) {
 
 template <int MODE, bool TEX>
 hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
-                          hipStream_t stream, int phase) {
+                          hipStream_t stream, int phase, int vis0) {
     if (fused) {
         if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
             hipLaunchKernelGGL((k_shade_fused<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L,
-                               W, b);
+                               W, b, vis0);
     } else if (phase == 0) {
-        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b);
+        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b,
+                           vis0);
     } else {
         hipLaunchKernelGGL((k_shade_b<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L, W,
-                           b);
+                           b, vis0);
     }
     return hipGetLastError();
 }
 
 template <int MODE>
-hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int cus,
-                        int items, hipStream_t stream, int phase) {
-    (void)cus;
-    return S.texinfo ? launch_shade_t<MODE, true>(fused, S, L, W, b, items, stream, phase)
-                     : launch_shade_t<MODE, false>(fused, S, L, W, b, items, stream, phase);
+hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
+                        hipStream_t stream, int phase, int vis0) {
+    return S.texinfo ? launch_shade_t<MODE, true>(fused, S, L, W, b, items, stream, phase, vis0)
+                     : launch_shade_t<MODE, false>(fused, S, L, W, b, items, stream, phase, vis0);
 }
 
+// vis0: n_lights when the bounce-0 (pixel, light) visibility table is used at this bounce, else 0
 hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b,
-                             int cus, int items, hipStream_t stream, int phase) {
+                             int items, hipStream_t stream, int phase, int vis0) {
     switch (mode) {
-        case kModeLambert: return launch_shade<kModeLambert>(fused, S, L, W, b, cus, items, stream, phase);
-        case kModeConductor: return launch_shade<kModeConductor>(fused, S, L, W, b, cus, items, stream, phase);
-        case kModeDielectric: return launch_shade<kModeDielectric>(fused, S, L, W, b, cus, items, stream, phase);
-        case kModeLayered: return launch_shade<kModeLayered>(fused, S, L, W, b, cus, items, stream, phase);
-        default: return launch_shade<kModeDefault>(fused, S, L, W, b, cus, items, stream, phase);
+        case kModeLambert: return launch_shade<kModeLambert>(fused, S, L, W, b, items, stream, phase, vis0);
+        case kModeConductor: return launch_shade<kModeConductor>(fused, S, L, W, b, items, stream, phase, vis0);
+        case kModeDielectric: return launch_shade<kModeDielectric>(fused, S, L, W, b, items, stream, phase, vis0);
+        case kModeLayered: return launch_shade<kModeLayered>(fused, S, L, W, b, items, stream, phase, vis0);
+        default: return launch_shade<kModeDefault>(fused, S, L, W, b, items, stream, phase, vis0);
     }
 }
 
@@ -770,25 +815,49 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         ++timed;
         return hipGetLastError();
     };
+    auto shadow_vis = [&](int b) -> hipError_t {
+        if (tex)
+            hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0, stream,
+                               S, W, b, L.counters);
+        else
+            hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockWF), 0,
+                               stream, S, W, b, L.counters);
+        return hipGetLastError();
+    };
+    // bounce-0 shadow dedup: one shadow ray per (pixel, light) instead of one per path; pays
+    // off while the batch has at least as many frames as there are lights
+    const int P1 = L.width * L.height;
+    const int vis0 = (primary_dedup && nf > 1 && L.n_lights >= 1 && L.n_lights <= nf) ? L.n_lights : 0;
+    auto shadow0 = [&]() -> hipError_t {
+        if (!vis0) return hipSuccess;
+        if (tex)
+            hipLaunchKernelGGL(k_shadow0_setup<true>, item_grid(P1 * vis0, kBlockWF), dim3(kBlockWF), 0, stream, S, L,
+                               W);
+        else
+            hipLaunchKernelGGL(k_shadow0_setup<false>, item_grid(P1 * vis0, kBlockWF), dim3(kBlockWF), 0, stream, S,
+                               L, W);
+        hipError_t r = hipGetLastError();
+        if (r != hipSuccess || (r = shadow_vis(0)) != hipSuccess) return r;
+        // the table's rays must not be traced again as bounce-0 shadow rays
+        return hipMemsetAsync(W.count + kShadowQ * kCntStride, 0, sizeof(int), stream);
+    };
     if (fused) {
         // extend(0); then per bounce: shade(b) -> [shadow rays of b + extension rays of b+1]
         if ((e = extend(0, primary_dedup ? nf : 1)) != hipSuccess) return e;
+        if ((e = shadow0()) != hipSuccess) return e;
         for (int b = 0; b < maxb; ++b) {
-            if ((e = launch_shade_mode(mode, true, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
+            if ((e = launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0)) != hipSuccess)
+                return e;
             if ((e = pair(b)) != hipSuccess) return e;
         }
     } else {
         for (int b = 0; b < maxb; ++b) {
             if ((e = extend(b, b == 0 && primary_dedup ? nf : 1)) != hipSuccess) return e;
-            if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 0)) != hipSuccess) return e;
-            if (tex)
-                hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0,
-                                   stream, S, W, b, L.counters);
-            else
-                hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockWF), 0,
-                                   stream, S, W, b, L.counters);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = launch_shade_mode(mode, false, S, L, W, b, cus, P, stream, 1)) != hipSuccess) return e;
+            const int v0 = b == 0 ? vis0 : 0;
+            if (v0 && (e = shadow0()) != hipSuccess) return e;
+            if ((e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 0, v0)) != hipSuccess) return e;
+            if (!v0 && (e = shadow_vis(b)) != hipSuccess) return e;
+            if ((e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 1, v0)) != hipSuccess) return e;
         }
     }
     hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
