@@ -290,12 +290,12 @@ __device__ __forceinline__ bool continue_path(const SurfaceHit& sf, const BSampl
 
 // Bounce-0 shadow dedup (with primary dedup): a pixel's first hit is the same in every frame
 // of the batch, so its shadow ray toward light li is too.  k_shadow0_setup builds one shadow
-// ray per (pixel, light) from the frame-0 hit, k_shadow_vis traces them into W.vis[pixel *
-// n_lights + light], and the bounce-0 shading reads that table instead of tracing a shadow ray
+// ray per (pixel, light) from the frame-0 hit, k_shadow_vis traces them into W.vis[light *
+// pixels + pixel], and the bounce-0 shading reads that table instead of tracing a shadow ray
 // per path.  Same rays, same any-hit answers: the images stay bit-identical.
 __device__ __forceinline__ int vis0_index(const DevLaunch& L, int path, int li) {
     const int P1 = L.width * L.height;
-    return (path % P1) * L.n_lights + li;  // path = frame * P1 + pixel
+    return li * P1 + path % P1;  // light-major (coherent shadow rays); path = frame * P1 + pixel
 }
 
 template <bool TEX>
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
     const int nl = L.n_lights;
     const int n = P1 * nl;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const int p = k / nl, li = k - p * nl;
+        const int li = k / P1, p = k - li * P1;
         const Hit h = decode_hit(W.hit[p]);  // frame 0's copy (queue 0 is in path order)
         float4 so = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(k)), sd = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
         if (h.tri >= 0) {  // same arithmetic as the shading kernels' shadow rays
