@@ -388,28 +388,46 @@ __device__ __forceinline__ bool trav_step_single(const DevScene& S, TravState& s
 #ifndef PT_NODE_SIGNSEL
 #define PT_NODE_SIGNSEL 1
 #endif
+#ifndef PT_LOAD_FIRST
+#define PT_LOAD_FIRST 0  // 1: a dual step issues its triangle and node loads before either test (slower)
+#endif
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
-// Slab test of the four children of node `ni`, hits as (t_near, child) with misses and
-// empty slots as kEmptyChild.  PT_NODE_SIGNSEL: the ray's direction signs pick the near and
-// far plane of every axis at load time (per-lane byte offsets into the node), so each child
-// needs no min/max per axis, and the plane distances are two children per packed v_pk_fma.
-// The planes are the same ones min/max would choose (fma is monotone in the plane
-// coordinate), so the result equals slab()'s.
-__device__ __forceinline__ void node_test(const DevScene& S, const TravState& s, int ni, float& t0, float& t1,
-                                          float& t2, float& t3, int& c0, int& c1, int& c2, int& c3) {
-    bool h0, h1, h2, h3;
-#if PT_NODE_SIGNSEL
+// The six sign-selected planes and the child links of one node, as loaded (PT_NODE_SIGNSEL).
+struct NodeLoad {
+    float4 ax, bx, ay, by, az, bz;
+    int4 ch;
+};
+
+__device__ __forceinline__ NodeLoad node_load(const DevScene& S, const TravState& s, int ni) {
     // raw buffer loads: one 32-bit offset add per plane instead of a 64-bit address
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.nodes, 0, 0x7fffffff, 0x00020000);
     const int nb = ni << 7;
     auto ld = [&](int off) {
         return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + off, 0, 0));
     };
-    const float4 ax = ld(s.nx), bx = ld(16 - s.nx);
-    const float4 ay = ld(32 + s.ny), by = ld(48 - s.ny);
-    const float4 az = ld(64 + s.nz), bz = ld(80 - s.nz);
-    const int4 ch = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + 96, 0, 0));
+    NodeLoad n;
+    n.ax = ld(s.nx);
+    n.bx = ld(16 - s.nx);
+    n.ay = ld(32 + s.ny);
+    n.by = ld(48 - s.ny);
+    n.az = ld(64 + s.nz);
+    n.bz = ld(80 - s.nz);
+    n.ch = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + 96, 0, 0));
+    return n;
+}
+
+// Slab test of the four children of a loaded node, hits as (t_near, child) with misses and
+// empty slots as kEmptyChild.  The ray's direction signs picked the near and far plane of
+// every axis at load time (per-lane byte offsets into the node), so each child needs no
+// min/max per axis, and the plane distances are two children per packed v_pk_fma.  The
+// planes are the same ones min/max would choose (fma is monotone in the plane coordinate),
+// so the result equals slab()'s.
+__device__ __forceinline__ void node_eval(const NodeLoad& n, const TravState& s, float& t0, float& t1, float& t2,
+                                          float& t3, int& c0, int& c1, int& c2, int& c3) {
+    bool h0, h1, h2, h3;
+    const float4 ax = n.ax, bx = n.bx, ay = n.ay, by = n.by, az = n.az, bz = n.bz;
+    const int4 ch = n.ch;
     const pt_f2 ix = {s.inv.x, s.inv.x}, iy = {s.inv.y, s.inv.y}, iz = {s.inv.z, s.inv.z};
     const pt_f2 ox = {-s.io.x, -s.io.x}, oy = {-s.io.y, -s.io.y}, oz = {-s.io.z, -s.io.z};
     const pt_f2 nx01 = __builtin_elementwise_fma(pt_f2{ax.x, ax.y}, ix, ox);
@@ -447,7 +465,15 @@ __device__ __forceinline__ void node_test(const DevScene& S, const TravState& s,
     c1 = h1 ? ch.y : kEmptyChild;
     c2 = h2 ? ch.z : kEmptyChild;
     c3 = h3 ? ch.w : kEmptyChild;
+}
+
+// Slab test of the four children of node `ni` (PT_NODE_SIGNSEL: node_load + node_eval).
+__device__ __forceinline__ void node_test(const DevScene& S, const TravState& s, int ni, float& t0, float& t1,
+                                          float& t2, float& t3, int& c0, int& c1, int& c2, int& c3) {
+#if PT_NODE_SIGNSEL
+    node_eval(node_load(S, s, ni), s, t0, t1, t2, t3, c0, c1, c2, c3);
 #else
+    bool h0, h1, h2, h3;
     const BNode4& n = S.nodes[ni];
     const int4 ch = n.child;
     const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
@@ -469,11 +495,11 @@ __device__ __forceinline__ void node_test(const DevScene& S, const TravState& s,
 
 // Test one triangle of the leaf s.leaf and advance it; true when an any-hit ray is done.
 template <int ANY, bool STATS, bool TEX>
-__device__ __forceinline__ bool leaf_tri_step(const DevScene& S, TravState& s, TravStats& ts) {
+__device__ __forceinline__ bool leaf_tri_eval(const DevScene& S, TravState& s, TravStats& ts, const float4 A,
+                                              const float4 E1, const float4 E2) {
     const int first = leaf_first(s.leaf), cnt = leaf_count(s.leaf);
     const int ti = first;
     if (STATS) ts.tris++;
-    const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
     float t, u, v;
     bool bk;
     bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
@@ -498,6 +524,12 @@ __device__ __forceinline__ bool leaf_tri_step(const DevScene& S, TravState& s, T
         s.h.orig = take ? oi : s.h.orig;
     }
     return false;
+}
+
+template <int ANY, bool STATS, bool TEX>
+__device__ __forceinline__ bool leaf_tri_step(const DevScene& S, TravState& s, TravStats& ts) {
+    const int ti = leaf_first(s.leaf);
+    return leaf_tri_eval<ANY, STATS, TEX>(S, s, ts, S.isect[3 * ti], S.isect[3 * ti + 1], S.isect[3 * ti + 2]);
 }
 
 // Next stack entry into s.cur (kEmptyChild when the stack is empty).
@@ -525,6 +557,23 @@ template <int ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                           int* spill, TravStats& ts, bool tri_ok = true) {
 #if PT_DUAL_STEP
+#if PT_LOAD_FIRST && PT_NODE_SIGNSEL
+    // issue the triangle's and the node's loads together (unconditional, clamped to valid
+    // records), so the two L2 round trips of a step overlap instead of following each other
+    const bool do_tri = tri_ok && s.leaf != kEmptyChild;
+    const bool do_node = s.cur >= 0;
+    const int tl = do_tri ? leaf_first(s.leaf) : 0;
+    const float4 TA = S.isect[3 * tl], TE1 = S.isect[3 * tl + 1], TE2 = S.isect[3 * tl + 2];
+    const NodeLoad nl = node_load(S, s, do_node ? s.cur : 0);
+    if (do_tri) {
+        if (leaf_tri_eval<ANY, STATS, TEX>(S, s, ts, TA, TE1, TE2)) return true;
+    }
+    if (do_node) {
+        if (STATS) ts.nodes++;
+        float t0, t1, t2, t3;
+        int c0, c1, c2, c3;
+        node_eval(nl, s, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
+#else
     if (tri_ok && s.leaf != kEmptyChild) {
         if (leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
     }
@@ -533,6 +582,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         float t0, t1, t2, t3;
         int c0, c1, c2, c3;
         node_test(S, s, s.cur, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
+#endif
         if ((ANY != kRayAny || !PT_ANY_UNSORTED) && PT_CHILD_SORT > 0) {
             cswap(t0, c0, t1, c1);
             cswap(t2, c2, t3, c3);
