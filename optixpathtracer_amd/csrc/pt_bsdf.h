@@ -385,6 +385,59 @@ __device__ __forceinline__ float dielectric_pdf(float roughness, f3 wo, f3 wi, b
     return tr_pdf(wo, wm, alpha) * dwm_dwi * pt / (pr + pt);
 }
 
+// dielectric_f and dielectric_pdf at the same (wo, wi) in one pass: the half vector, the
+// Fresnel term, D(wm) and the two Smith lambdas are computed once.  Each output keeps the
+// arithmetic of its own function (tr_G = 1 / ((1 + L(wo)) + L(wi)), tr_pdf = G1(wo) / |cos wo|
+// * D * |wo.wm|), so both are bit-identical to the separate calls; the layered walk evaluates
+// f and pdf of one interface together at every NEE step (GlossyDiffuse.h:318-329, :342-352).
+__device__ __forceinline__ void dielectric_f_pdf(float roughness, f3 wo, f3 wi, int mode, bool reflection,
+                                                 bool transmission, float& f, float& pdf) {
+    const float eta = 1.5f;
+    f = 0.0f;
+    pdf = 0.0f;
+    float alpha = sqr(roughness);
+    if (alpha < 1e-3f) return;
+    float co = wo.z, ci = wi.z;
+    bool reflect = ci * co > 0.0f;
+    float etap = 1.0f;
+    if (!reflect) etap = co > 0.0f ? eta : (1.0f / eta);
+    f3 wm = wi * etap + wo;
+    if (ci == 0.0f || co == 0.0f) return;
+    const bool f_ok = sqr(length(wm)) != 0.0f;  // dielectric_f's test
+    const bool p_ok = length_sqr(wm) != 0.0f;   // dielectric_pdf's test
+    if (!f_ok && !p_ok) return;
+    wm = faceforward_z(wm);
+    if (dot(wm, wi) * ci < 0.0f || dot(wm, wo) * co < 0.0f) return;
+    const float F = fresnel_dielectric(dot(wo, wm), eta);
+    const float D = tr_D(wm, alpha);
+    const float lo = tr_lambda(wo, alpha), li = tr_lambda(wi, alpha);
+    const float G = 1.0f / (1.0f + lo + li);
+    const float tp = (1.0f / (1.0f + lo)) / abs_cos_theta(wo) * D * abs_dot(wo, wm);
+    float fv, pv;
+    if (reflect) {
+        fv = D * G * F / fabsf(4.0f * ci * co);
+    } else {
+        float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap) * ci * co;
+        fv = D * (1.0f - F) * G * fabsf(dot(wi, wm) * dot(wo, wm) / denom);
+        if (mode == kRadiance) fv /= sqr(etap);
+    }
+    const float R = F, T = 1.0f - R;
+    float pr = R, pt = T;
+    if (!reflection) pr = 0.0f;
+    if (!transmission) pt = 0.0f;
+    if (pr == 0.0f && pt == 0.0f) {
+        pv = 0.0f;
+    } else if (reflect) {
+        pv = tp / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
+    } else {
+        float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
+        float dwm_dwi = abs_dot(wi, wm) / denom;
+        pv = tp * dwm_dwi * pt / (pr + pt);
+    }
+    f = f_ok ? fv : 0.0f;
+    pdf = p_ok ? pv : 0.0f;
+}
+
 // ---- Layered "GlossyDiffuse" (dielectric top, Lambert bottom): GlossyDiffuse.h:91-524 ------
 __device__ __forceinline__ float power_heuristic(float fpdf, float gpdf) {  // :91-95 (nf=ng=1)
     float f = 1.0f * fpdf, g = 1.0f * gpdf;
@@ -409,6 +462,18 @@ __device__ __forceinline__ bool layer_sample(bool top, uint32_t& seed, f3 albedo
 __device__ __forceinline__ float layer_pdf(bool top, float roughness, f3 wo, f3 wi, bool refl, bool trans) {
     return top ? dielectric_pdf(roughness, wo, wi, refl, trans) : lambert_pdf(wo, wi, refl);
 }
+// layer_f and layer_pdf of one interface at the same directions (PT_LAYERED_FUSE)
+__device__ __forceinline__ void layer_f_pdf(bool top, f3 albedo, float roughness, f3 wo, f3 wi, int mode, bool refl,
+                                            bool trans, f3& f, float& pdf) {
+    if (top) {
+        float v;
+        dielectric_f_pdf(roughness, wo, wi, mode, refl, trans, v, pdf);
+        f = mk(v, v, v);
+    } else {
+        f = lambert_f(albedo, wo, wi);
+        pdf = lambert_pdf(wo, wi, refl);
+    }
+}
 __device__ __forceinline__ bool bs_bad(bool ok, const BSample& b) {
     return !ok || is_zero(b.color) || b.pdf == 0.0f || b.dir.z == 0.0f;
 }
@@ -417,6 +482,9 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
     return mk(b.color.x * c / b.pdf, b.color.y * c / b.pdf, b.color.z * c / b.pdf);
 }
 
+#ifndef PT_LAYERED_FUSE
+#define PT_LAYERED_FUSE 1  // fused f + pdf per interface, hoisted transmittances (bit-identical)
+#endif
 #ifndef PT_LAYERED_INLINE
 #define PT_LAYERED_INLINE 0
 #endif
@@ -461,6 +529,11 @@ __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughne
         f3 beta = bs_weight(wos);
         float z = enteredTop ? thickness : 0.0f;
         f3 w = wos.dir;
+#if PT_LAYERED_FUSE
+        // loop-invariant / carried transmittances: the same calls on the same directions
+        const float tr_wis = transmittance(thickness, wis.dir);
+        float tr_w = transmittance(thickness, w);
+#endif
         for (int depth = 0; depth < 10; ++depth) {
             if (depth > 3 && save_max(beta) < 0.25f) {
                 float q = gmax(0.0f, 1.0f - save_max(beta));
@@ -468,7 +541,11 @@ __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughne
                 beta = beta / (1.0f - q);
             }
             z = (z == thickness) ? 0.0f : thickness;
+#if PT_LAYERED_FUSE
+            beta = beta * tr_w;
+#else
             beta = beta * transmittance(thickness, w);
+#endif
             // The reference branches on z == exitZ (GlossyDiffuse.h:315-360); lanes of a wave
             // disagree on exitZ, so both branches would run every depth.  Here the two
             // layer_sample calls are one call on the selected layer, with the NEE terms of the
@@ -478,11 +555,19 @@ __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughne
             const bool atExit = z == exitZ;
             if (!atExit && !nonExitSpec) {
                 float wt = 1.0f;
+#if PT_LAYERED_FUSE
+                f3 lf;
+                float lpdf;
+                layer_f_pdf(nonExitTop, albedo, roughness, -w, -wis.dir, mode, true, true, lf, lpdf);
+                if (!exitSpec) wt = power_heuristic(wis.pdf, lpdf);
+                const float tr = tr_wis;
+#else
                 if (!exitSpec)
                     wt = power_heuristic(wis.pdf, layer_pdf(nonExitTop, roughness, -w, -wis.dir, true, true));
                 f3 lf = layer_f(nonExitTop, albedo, roughness, -w, -wis.dir, mode);
-                float ac = abs_cos_theta(wis.dir);
                 float tr = transmittance(thickness, wis.dir);
+#endif
+                float ac = abs_cos_theta(wis.dir);
                 f3 t1 = beta * lf;
                 t1 = t1 * ac;
                 t1 = t1 * wt;
@@ -495,12 +580,24 @@ __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughne
             if (bs_bad(ok, bs)) break;
             beta = beta * bs_weight(bs);
             w = bs.dir;
+#if PT_LAYERED_FUSE
+            tr_w = transmittance(thickness, w);  // this NEE term's and the next depth's factor
+            if (!atExit && !exitSpec) {
+                f3 fExit;
+                float epdf;
+                layer_f_pdf(exitTop, albedo, roughness, -w, wi, mode, false, true, fExit, epdf);
+                if (!is_zero(fExit)) {
+                    float wt = 1.0f;
+                    if (!nonExitSpec) wt = power_heuristic(bs.pdf, epdf);
+                    const float tr = tr_w;
+#else
             if (!atExit && !exitSpec) {
                 f3 fExit = layer_f(exitTop, albedo, roughness, -w, wi, mode);
                 if (!is_zero(fExit)) {
                     float wt = 1.0f;
                     if (!nonExitSpec) wt = power_heuristic(bs.pdf, layer_pdf(exitTop, roughness, -w, wi, false, true));
                     float tr = transmittance(thickness, bs.dir);
+#endif
                     f3 t1 = beta * tr;
                     t1 = t1 * fExit;
                     t1 = t1 * wt;

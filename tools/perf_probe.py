@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--spp", type=int, default=16)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--modes", default="")
-    ap.add_argument("--kernels", default="0")
+    ap.add_argument("--kernels", default="2", help="0 = megakernel, 1 = wavefront, 2 = auto")
     ap.add_argument("--fpl", default="8")
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--repeat", type=int, default=2)
