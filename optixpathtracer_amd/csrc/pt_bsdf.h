@@ -93,11 +93,29 @@ __device__ __forceinline__ float tr_G1(f3 w, float alpha) { return 1.0f / (1.0f 
 __device__ __forceinline__ float tr_pdf(f3 w, f3 wm, float alpha) {   // D(w, wm): :81-88
     return tr_G1(w, alpha) / abs_cos_theta(w) * tr_D(wm, alpha) * abs_dot(w, wm);
 }
-__device__ __forceinline__ f3 tr_sample_wm(uint32_t& seed, f3 w, float alpha) {  // :90-119
+// Trowbridge-Reitz quantities of one direction w that every sample or evaluation with w as
+// the outgoing direction recomputes: tr_sample_wm's hemisphere frame, Lambda(w) and
+// G1(w) / |cos w|.  The layered walk computes them once per direction and reuses them across
+// its samples and depths; they are the same operations on the same inputs, so every result
+// stays bit-identical to recomputing them inline.
+struct TRDir {
+    f3 wh, T1, T2;  // tr_sample_wm frame (tr_dir_frame)
+    float lam;      // tr_lambda(w, alpha) (tr_dir_lam)
+    float g1c;      // tr_G1(w, alpha) / abs_cos_theta(w) (tr_dir_lam)
+};
+__device__ __forceinline__ void tr_dir_lam(TRDir& p, f3 w, float alpha) {
+    p.lam = tr_lambda(w, alpha);
+    p.g1c = (1.0f / (1.0f + p.lam)) / abs_cos_theta(w);
+}
+__device__ __forceinline__ void tr_dir_frame(TRDir& p, f3 w, float alpha) {  // Microfacet.h:90-98
     f3 wh = normalize(mk(alpha * w.x, alpha * w.y, w.z));
     if (wh.z < 0.0f) wh = -wh;
-    f3 T1 = (wh.z < 0.99999f) ? normalize(cross(mk(0.0f, 0.0f, 1.0f), wh)) : mk(1.0f, 0.0f, 0.0f);
-    f3 T2 = cross(wh, T1);
+    p.T1 = (wh.z < 0.99999f) ? normalize(cross(mk(0.0f, 0.0f, 1.0f), wh)) : mk(1.0f, 0.0f, 0.0f);
+    p.T2 = cross(wh, p.T1);
+    p.wh = wh;
+}
+__device__ __forceinline__ f3 tr_sample_wm_dir(uint32_t& seed, const TRDir& p, float alpha) {  // :99-119
+    const f3 wh = p.wh, T1 = p.T1, T2 = p.T2;
     float px, py;
     disk_polar(seed, px, py);
     float h = sqrtf(1.0f - sqr(px));
@@ -107,6 +125,11 @@ __device__ __forceinline__ f3 tr_sample_wm(uint32_t& seed, f3 w, float alpha) { 
     f3 nh = mk(px * T1.x + py * T2.x + pz * wh.x, px * T1.y + py * T2.y + pz * wh.y,
                px * T1.z + py * T2.z + pz * wh.z);
     return normalize(mk(alpha * nh.x, alpha * nh.y, gmax(1e-6f, nh.z)));
+}
+__device__ __forceinline__ f3 tr_sample_wm(uint32_t& seed, f3 w, float alpha) {  // :90-119
+    TRDir p;
+    tr_dir_frame(p, w, alpha);
+    return tr_sample_wm_dir(seed, p, alpha);
 }
 
 // ---- Conductor: Conductor.h:42-190, Complex.h:5-63 ---------------------------------------
@@ -284,9 +307,10 @@ __device__ __forceinline__ float dielectric_f(float roughness, f3 wo, f3 wi, int
     if (mode == kRadiance) ft /= sqr(etap);
     return ft;
 }
-__device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughness, f3 wo, BSample& s,
-                                                  int mode, bool reflection, bool transmission) {
-    // :146-288
+// Dielectric.h:146-288 with the wo-only Trowbridge-Reitz terms taken from `p` (a full TRDir of
+// wo when the surface is rough; unused when smooth).
+__device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roughness, f3 wo, const TRDir& p,
+                                                      BSample& s, int mode, bool reflection, bool transmission) {
     const float eta = 1.5f;
     float alpha = sqr(roughness);
     float uc = rnd(seed);  // drawn first, always (:149)
@@ -321,7 +345,7 @@ __device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughnes
         s.spec = true;
         return true;
     }
-    f3 wm = tr_sample_wm(seed, wo, alpha);
+    f3 wm = tr_sample_wm_dir(seed, p, alpha);
     float R = fresnel_dielectric(dot(wo, wm), eta);
     float T = 1.0f - R;
     float pr = R, pt = T;
@@ -333,8 +357,8 @@ __device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughnes
         float d = dot(wm, I);
         f3 wi = mk(I.x - wm.x * d * 2.0f, I.y - wm.y * d * 2.0f, I.z - wm.z * d * 2.0f);
         if (!same_hemisphere(wo, wi)) return false;
-        float pdf = tr_pdf(wo, wm, alpha) / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
-        float f = tr_D(wm, alpha) * tr_G(wo, wi, alpha) * R / (4.0f * wi.z * wo.z);
+        float pdf = p.g1c * tr_D(wm, alpha) * abs_dot(wo, wm) / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
+        float f = tr_D(wm, alpha) * (1.0f / (1.0f + p.lam + tr_lambda(wi, alpha))) * R / (4.0f * wi.z * wo.z);
         s.color = mk(f, f, f);
         s.dir = wi;
         s.pdf = pdf;
@@ -349,8 +373,8 @@ __device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughnes
     if (tir || same_hemisphere(wo, wi) || wi.z == 0.0f) return false;
     float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
     float dwm_dwi = abs_dot(wi, wm) / denom;
-    float pdf = tr_pdf(wo, wm, alpha) * dwm_dwi * pt / (pr + pt);
-    float ft = T * tr_D(wm, alpha) * tr_G(wo, wi, alpha) * fabsf(dot(wi, wm) * dot(wo, wm) / (wi.z * wo.z * denom));
+    float pdf = p.g1c * tr_D(wm, alpha) * abs_dot(wo, wm) * dwm_dwi * pt / (pr + pt);
+    float ft = T * tr_D(wm, alpha) * (1.0f / (1.0f + p.lam + tr_lambda(wi, alpha))) * fabsf(dot(wi, wm) * dot(wo, wm) / (wi.z * wo.z * denom));
     if (mode == kRadiance) ft /= sqr(etap);
     s.color = mk(ft, ft, ft);
     s.dir = wi;
@@ -359,6 +383,16 @@ __device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughnes
     s.trans = true;
     s.spec = false;
     return true;
+}
+__device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughness, f3 wo, BSample& s,
+                                                  int mode, bool reflection, bool transmission) {
+    TRDir p{};
+    const float alpha = sqr(roughness);
+    if (!(alpha < 1e-3f)) {
+        tr_dir_frame(p, wo, alpha);
+        tr_dir_lam(p, wo, alpha);
+    }
+    return dielectric_sample_dir(seed, roughness, wo, p, s, mode, reflection, transmission);
 }
 __device__ __forceinline__ float dielectric_pdf(float roughness, f3 wo, f3 wi, bool reflection,
                                                 bool transmission) {  // :290-343
@@ -390,8 +424,10 @@ __device__ __forceinline__ float dielectric_pdf(float roughness, f3 wo, f3 wi, b
 // arithmetic of its own function (tr_G = 1 / ((1 + L(wo)) + L(wi)), tr_pdf = G1(wo) / |cos wo|
 // * D * |wo.wm|), so both are bit-identical to the separate calls; the layered walk evaluates
 // f and pdf of one interface together at every NEE step (GlossyDiffuse.h:318-329, :342-352).
-__device__ __forceinline__ void dielectric_f_pdf(float roughness, f3 wo, f3 wi, int mode, bool reflection,
-                                                 bool transmission, float& f, float& pdf) {
+// `po` holds lam / g1c of wo (tr_dir_lam), `lam_i` = tr_lambda(wi, alpha).
+__device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, const TRDir& po, f3 wi, float lam_i,
+                                                     int mode, bool reflection, bool transmission, float& f,
+                                                     float& pdf) {
     const float eta = 1.5f;
     f = 0.0f;
     pdf = 0.0f;
@@ -410,9 +446,8 @@ __device__ __forceinline__ void dielectric_f_pdf(float roughness, f3 wo, f3 wi, 
     if (dot(wm, wi) * ci < 0.0f || dot(wm, wo) * co < 0.0f) return;
     const float F = fresnel_dielectric(dot(wo, wm), eta);
     const float D = tr_D(wm, alpha);
-    const float lo = tr_lambda(wo, alpha), li = tr_lambda(wi, alpha);
-    const float G = 1.0f / (1.0f + lo + li);
-    const float tp = (1.0f / (1.0f + lo)) / abs_cos_theta(wo) * D * abs_dot(wo, wm);
+    const float G = 1.0f / (1.0f + po.lam + lam_i);
+    const float tp = po.g1c * D * abs_dot(wo, wm);
     float fv, pv;
     if (reflect) {
         fv = D * G * F / fabsf(4.0f * ci * co);
@@ -436,6 +471,13 @@ __device__ __forceinline__ void dielectric_f_pdf(float roughness, f3 wo, f3 wi, 
     }
     f = f_ok ? fv : 0.0f;
     pdf = p_ok ? pv : 0.0f;
+}
+__device__ __forceinline__ void dielectric_f_pdf(float roughness, f3 wo, f3 wi, int mode, bool reflection,
+                                                 bool transmission, float& f, float& pdf) {
+    TRDir po;
+    const float alpha = sqr(roughness);
+    tr_dir_lam(po, wo, alpha);
+    dielectric_f_pdf_dir(roughness, wo, po, wi, tr_lambda(wi, alpha), mode, reflection, transmission, f, pdf);
 }
 
 // ---- Layered "GlossyDiffuse" (dielectric top, Lambert bottom): GlossyDiffuse.h:91-524 ------
@@ -483,7 +525,9 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
 }
 
 #ifndef PT_LAYERED_FUSE
-#define PT_LAYERED_FUSE 1  // fused f + pdf per interface, hoisted transmittances (bit-identical)
+// 1: fused f + pdf per interface and hoisted transmittances; 2: + per-direction Trowbridge-Reitz
+// terms computed once (TRDir).  All levels give bit-identical results (tools/render_npy.py).
+#define PT_LAYERED_FUSE 2
 #endif
 #ifndef PT_LAYERED_INLINE
 #define PT_LAYERED_INLINE 0
@@ -493,6 +537,148 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
 #else
 #define PT_LAYERED_ATTR __noinline__
 #endif
+#if PT_LAYERED_FUSE >= 2
+__device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+    // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code).
+    // The top interface is the rough or smooth dielectric, the bottom the Lambertian.  Terms
+    // that depend on one direction only are computed once per direction (TRDir): wo and wi
+    // for the whole walk, -w from the exit NEE term of one depth for the sample of the next
+    // (same direction), so every value is the one the inline calls would produce.
+    const int mode = kRadiance;
+    const float thickness = 0.01f;
+    const float alpha = sqr(roughness);
+    const bool topSpec = alpha < 1e-3f;
+    const bool botSpec = false;
+    f3 f = mk(0, 0, 0);
+    if (wo.z < 0.0f) {
+        wo = -wo;
+        wi = -wi;
+    }
+    const bool enteredTop = true;
+    const bool same = same_hemisphere(wo, wi);
+    bool exitTop, nonExitTop, exitSpec, nonExitSpec;
+    if (same ^ enteredTop) {
+        exitSpec = botSpec; nonExitSpec = topSpec; exitTop = false; nonExitTop = true;
+    } else {
+        exitSpec = topSpec; nonExitSpec = botSpec; exitTop = true; nonExitTop = false;
+    }
+    const float exitZ = (same ^ enteredTop) ? 0.0f : thickness;
+    TRDir pwo{}, pwi{};
+    if (!topSpec) {
+        tr_dir_frame(pwo, wo, alpha);
+        tr_dir_lam(pwo, wo, alpha);
+        if (exitTop) {
+            tr_dir_frame(pwi, wi, alpha);
+            tr_dir_lam(pwi, wi, alpha);
+        }
+    }
+    if (same) {  // layer_f(enteredTop = top, wo, wi)
+        float v, unused;
+        dielectric_f_pdf_dir(roughness, wo, pwo, wi, pwi.lam, mode, true, true, v, unused);
+        f = mk(5.0f, 5.0f, 5.0f) * mk(v, v, v);
+    }
+
+    uint32_t ns = tea16(f2u_sat(wo.x * 1000.0f), f2u_sat(wo.y * 1000.0f));
+    ns = tea16(ns, f2u_sat(wi.x * 1000.0f));
+    ns = tea16(ns, f2u_sat(wi.y * 1000.0f));
+    ns = tea16(ns, seed);
+
+    for (int s = 0; s < 5; ++s) {
+        BSample wos, wis, bs;
+        bool ok = dielectric_sample_dir(seed, roughness, wo, pwo, wos, mode, false, true);  // enteredTop
+        if (bs_bad(ok, wos)) continue;
+        ok = exitTop ? dielectric_sample_dir(seed, roughness, wi, pwi, wis, kImportance, false, true)
+                     : lambert_sample(seed, albedo, false, wis);
+        if (bs_bad(ok, wis)) continue;
+        f3 beta = bs_weight(wos);
+        float z = enteredTop ? thickness : 0.0f;
+        f3 w = wos.dir;
+        const float tr_wis = transmittance(thickness, wis.dir);
+        float tr_w = transmittance(thickness, w);
+        // NEE through the top as the non-exit interface (wi below the surface)
+        const float lam_nwis = (nonExitTop && !topSpec) ? tr_lambda(-wis.dir, alpha) : 0.0f;
+        TRDir cw{};  // lam / g1c (and, for a top sample, the frame) of -w
+        bool cw_ok = false;
+        for (int depth = 0; depth < 10; ++depth) {
+            if (depth > 3 && save_max(beta) < 0.25f) {
+                float q = gmax(0.0f, 1.0f - save_max(beta));
+                if (rnd(ns) < q) break;
+                beta = beta / (1.0f - q);
+            }
+            z = (z == thickness) ? 0.0f : thickness;
+            beta = beta * tr_w;
+            // The reference branches on z == exitZ (GlossyDiffuse.h:315-360); lanes of a wave
+            // disagree on exitZ, so both branches would run every depth.  Here the two
+            // layer_sample calls are one call on the selected layer, with the NEE terms of the
+            // non-exit branch predicated around it: the same operations and random numbers.
+            // (Flattening the sample and depth loops into one loop of steps, so lanes start
+            // their next sample early, was 40 % slower: DESIGN.md §5.)
+            const bool atExit = z == exitZ;
+            const bool itop = atExit ? exitTop : nonExitTop;
+            if (itop && !topSpec && !cw_ok) {
+                tr_dir_lam(cw, -w, alpha);
+                cw_ok = true;
+            }
+            if (!atExit && !nonExitSpec) {
+                float wt = 1.0f;
+                f3 lf;
+                float lpdf;
+                if (nonExitTop) {
+                    float v;
+                    dielectric_f_pdf_dir(roughness, -w, cw, -wis.dir, lam_nwis, mode, true, true, v, lpdf);
+                    lf = mk(v, v, v);
+                } else {
+                    lf = lambert_f(albedo, -w, -wis.dir);
+                    lpdf = lambert_pdf(-w, -wis.dir, true);
+                }
+                if (!exitSpec) wt = power_heuristic(wis.pdf, lpdf);
+                float ac = abs_cos_theta(wis.dir);
+                f3 t1 = beta * lf;
+                t1 = t1 * ac;
+                t1 = t1 * wt;
+                t1 = t1 * tr_wis;
+                t1 = t1 * wis.color;
+                t1 = t1 / wis.pdf;
+                f = f + t1;
+            }
+            if (itop) {
+                if (!topSpec) tr_dir_frame(cw, -w, alpha);
+                ok = dielectric_sample_dir(seed, roughness, -w, cw, bs, mode, true, false);
+            } else {
+                ok = lambert_sample(seed, albedo, true, bs);
+            }
+            if (bs_bad(ok, bs)) break;
+            beta = beta * bs_weight(bs);
+            w = bs.dir;
+            cw_ok = false;
+            tr_w = transmittance(thickness, w);  // this NEE term's and the next depth's factor
+            if (!atExit && !exitSpec) {
+                f3 fExit;
+                float epdf;
+                if (exitTop) {
+                    tr_dir_lam(cw, -w, alpha);  // reused by the next depth's top sample
+                    cw_ok = true;
+                    float v;
+                    dielectric_f_pdf_dir(roughness, -w, cw, wi, pwi.lam, mode, false, true, v, epdf);
+                    fExit = mk(v, v, v);
+                } else {
+                    fExit = lambert_f(albedo, -w, wi);
+                    epdf = lambert_pdf(-w, wi, false);
+                }
+                if (!is_zero(fExit)) {
+                    float wt = 1.0f;
+                    if (!nonExitSpec) wt = power_heuristic(bs.pdf, epdf);
+                    f3 t1 = beta * tr_w;
+                    t1 = t1 * fExit;
+                    t1 = t1 * wt;
+                    f = f + t1;
+                }
+            }
+        }
+    }
+    return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
+}
+#else
 __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
     // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code)
     const int mode = kRadiance;
@@ -608,6 +794,7 @@ __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughne
     }
     return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
 }
+#endif
 
 __device__ PT_LAYERED_ATTR bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
     // GlossyDiffuse.h:372-524
