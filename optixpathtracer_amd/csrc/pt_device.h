@@ -130,7 +130,10 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
 // slow flat load on every step).
 // The LDS depth is a template parameter (DEPTH): it trades LDS per workgroup against
 // occupancy per kernel (see pt_render.hip / pt_wavefront.hip).
-constexpr int kSpillDepth = 64;  // spill + LDS hold a BVH4 path of depth > 20
+#ifndef PT_SPILL_DEPTH
+#define PT_SPILL_DEPTH 64
+#endif
+constexpr int kSpillDepth = PT_SPILL_DEPTH;  // spill + LDS hold a BVH4 path of depth > 20
 #ifndef PT_DUAL_STEP
 #define PT_DUAL_STEP 1  // one node AND one triangle per traversal step (see trav_step)
 #endif

@@ -46,6 +46,9 @@ constexpr int kStack = PT_WF_STACK;
 #define PT_WF_WAVES 1
 #endif
 constexpr int kMissTri = -1;
+#ifndef PT_PAIR_SPECIALISE
+#define PT_PAIR_SPECIALISE 0  // 1: k_trace_pair runs shadow-only waves in an any-hit loop (slower)
+#endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
@@ -167,12 +170,10 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
-__device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TravStats& ts, Fetch fetch,
-                                            Finish finish) {
+__device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TravStats& ts,
+                                            Fetch fetch, Finish finish) {
     int spill[kSpillDepth];
     TravState st;
-    int next, end;
-    wave_slice(n, next, end);
     int ri = -1;
     while (true) {
         const bool need = ri < 0;
@@ -207,6 +208,14 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
             ri = -1;
         }
     }
+}
+
+template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
+__device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TravStats& ts, Fetch fetch,
+                                            Finish finish) {
+    int next, end;
+    wave_slice(n, next, end);
+    trace_range<ANY, STATS, TEX>(S, next, end, stk, ts, fetch, finish);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -416,9 +425,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
     const float4* rd = W.ray_d[(b + 1) & 1];
     int* stk = stack + threadIdx.x;
     TravStats ts;
-    trace_slice<kRayMixed, STATS, TEX>(
-        S, n_ext + n_sh, stk, ts,
-        [&](int i, TravState& st) {
+    auto fetch = [&](int i, TravState& st) {
             if (i < n_ext) {
                 const float4 a = ldq(ro + i), c = ldq(rd + i);
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
@@ -428,8 +435,8 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
                 st.any = true;
             }
-        },
-        [&](int i, const TravState& st) {
+        };
+    auto finish = [&](int i, const TravState& st) {
             const Hit& h = st.h;
             if (i < n_ext) {
                 stq(W.hit + i, h.tri >= 0 ? make_float4(h.t, h.u, h.v,
@@ -442,7 +449,23 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
                 const float4 l = W.L[path];
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
-        });
+        };
+    // The queue is [extension rays | shadow rays] and wave slices are contiguous, so all but
+    // one wave trace a single ray kind: those run a loop specialised to it (no child sort and
+    // no closest-hit bookkeeping for shadow rays, no any-hit tests for extension rays).
+    int first, end;
+    wave_slice(n_ext + n_sh, first, end);
+#if PT_PAIR_SPECIALISE
+    if (first >= n_ext)
+        trace_range<kRayAny, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
+    else
+#endif
+#if PT_PAIR_SPECIALISE > 1
+    if (end <= n_ext)
+        trace_range<kRayClosest, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
+    else
+#endif
+        trace_range<kRayMixed, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
