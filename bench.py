@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024, help="samples per pixel per GPU per step")
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--kernel", type=int, default=2, help="0 = megakernel, 1 = wavefront, 2 = auto")
-    ap.add_argument("--frames-per-launch", type=int, default=16)
+    ap.add_argument("--frames-per-launch", type=int, default=64)
     ap.add_argument("--no-dedup-check", action="store_true",
                     help="skip the extra step timed with pt_set_primary_dedup(0)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)

@@ -136,7 +136,7 @@ int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count);
 int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces);
 int pt_set_material_mode(pt_renderer* r, int32_t material_mode);
 int pt_set_kernel(pt_renderer* r, int32_t kernel);
-/* frames (spp) rendered per launch by pt_render_frames (default 16): the megakernel loops them in
+/* frames (spp) rendered per launch by pt_render_frames (default 64): the megakernel loops them in
    registers; the wavefront keeps all of their paths in flight in one kernel chain. */
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames);
 /* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */

@@ -46,6 +46,9 @@ constexpr int kStack = PT_WF_STACK;
 #define PT_WF_WAVES 1
 #endif
 constexpr int kMissTri = -1;
+#ifndef PT_SHADOW_CARRY
+#define PT_SHADOW_CARRY 1  // shadow rays carry path + contribution in the hit record (k_trace_pair)
+#endif
 #ifndef PT_PAIR_SPECIALISE
 #define PT_PAIR_SPECIALISE 0  // 1: k_trace_pair runs shadow-only waves in an any-hit loop (slower)
 #endif
@@ -434,6 +437,15 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
                 const float4 a = ldq(W.sh_o + j), c = ldq(W.sh_d + j);
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
                 st.any = true;
+#if PT_SHADOW_CARRY
+                // an any-hit traversal only writes h.tri / h.orig, and only when occluded: the
+                // record's free fields carry the path and the contribution to finish()
+                const float4 k = ldq(W.sh_c + j);
+                st.h.orig = __float_as_int(a.w);
+                st.h.t = k.x;
+                st.h.u = k.y;
+                st.h.v = k.z;
+#endif
             }
         };
     auto finish = [&](int i, const TravState& st) {
@@ -443,9 +455,14 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
                                                         __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
                                           : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri)));
             } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+#if PT_SHADOW_CARRY
+                const int path = h.orig;
+                const float4 k = make_float4(h.t, h.u, h.v, 0.0f);
+#else
                 const int j = i - n_ext;
                 const int path = __float_as_int(W.sh_o[j].w);
                 const float4 k = ldq(W.sh_c + j);
+#endif
                 const float4 l = W.L[path];
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
