@@ -66,7 +66,8 @@ def parse():
 
 def cpu_baseline(scene, args, budget_s: float):
     """The CPU oracle (oracle/liboracle.so, test/baseline infrastructure) on a band of the
-    same workload, on this host's cores; sized to ~budget_s of CPU work."""
+    same workload, on this host's cores; sized to ~budget_s of CPU work.  Returns the band's
+    radiance sum (rows, W, 3), its spp and the baseline record."""
     from oracle.oracle import OracleScene
 
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
@@ -80,11 +81,12 @@ def cpu_baseline(scene, args, budget_s: float):
     per_spp = max(time.perf_counter() - t, 1e-3)
     spp = int(max(1, min(args.spp, budget_s / per_spp)))
     t = time.perf_counter()
-    _, segs = o.render(lp, 1, spp, rect=(0, y0, args.width, y0 + rows), threads=threads)
+    band, segs = o.render(lp, 1, spp, rect=(0, y0, args.width, y0 + rows), threads=threads)
+    band = band[y0:y0 + rows]
     dt = time.perf_counter() - t
     samples = rows * args.width * spp
     o.close()
-    return {
+    return band, spp, {
         "value": round(samples / dt / 1e6, 4),
         "unit": "Msamples/sec",
         "cores": threads,
@@ -268,7 +270,21 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline (oracle) ...")
-            out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_baseline_seconds)
+            band, spp_cpu, out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_baseline_seconds)
+            # "MSE vs reference" of the metric: the GPU renders the same frame ids (1..spp_cpu)
+            # untimed, and its band is compared with the oracle's per-pixel mean radiance
+            r.accum_clear()
+            r.render_frames(1, spp_cpu)
+            r.synchronize()
+            gpu = accum.cpu().numpy()[args.height - band.shape[0]:].astype(np.float64) / spp_cpu
+            ref = band.astype(np.float64) / spp_cpu
+            diff = np.nan_to_num(gpu, nan=0.0) - np.nan_to_num(ref, nan=0.0)  # NaN -> 0 (WriteImage.cpp:52-55)
+            out["mse_vs_oracle"] = {
+                "mse": float(np.mean(diff * diff)),
+                "max_abs": float(np.max(np.abs(diff))),
+                "bar": 1e-5,
+                "sample": out["cpu_baseline"]["sample"].split(",")[0] + " (GPU render of the same frame ids)",
+            }
         print(json.dumps(out), flush=True)
     r.close()
     if dist is not None:

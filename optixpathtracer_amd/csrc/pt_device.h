@@ -140,6 +140,9 @@ constexpr int kSpillDepth = PT_SPILL_DEPTH;  // spill + LDS hold a BVH4 path of 
 #ifndef PT_TRI_PER_STEP
 #define PT_TRI_PER_STEP 1
 #endif
+#ifndef PT_SKIP_LAST_SAMPLE
+#define PT_SKIP_LAST_SAMPLE 1  // no BSDF sample on a path's last segment (its ray is never traced)
+#endif
 
 // ---- textures: devicePrograms.cu:62-73 (SRGB8ToLinear), :131-166 (GetTextureCoord,
 // SampleTextures), :518-543 (AlphaCutout); CreateTextures (OptixRenderer.cpp:562-612) sets up
@@ -216,6 +219,7 @@ struct TravState {
     int leaf;          // PT_DUAL_STEP: leaf whose triangles are tested alongside node steps
     int nx, ny, nz;    // byte offset (0 or 16) of the near slab plane per axis within the node
     bool any;          // any-hit ray (only read by kRayMixed traversals)
+    int path;          // wavefront extension rays: the path id, for the hit record
     Hit h;
 };
 
@@ -815,6 +819,12 @@ __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch&
         }
     }
     BSample bs;
+    // the last segment's sampled direction is never traced (SamplePath's loop test, :646):
+    // skipping the sample leaves every traced value unchanged
+    if (PT_SKIP_LAST_SAMPLE && p.bounce >= L.max_bounces) {
+        p.end = true;
+        return;
+    }
     if (!bsdf_sample<MODE>(p.seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
         p.end = true;
         return;

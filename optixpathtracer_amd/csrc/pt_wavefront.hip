@@ -49,11 +49,23 @@ constexpr int kMissTri = -1;
 #ifndef PT_SHADOW_CARRY
 #define PT_SHADOW_CARRY 1  // shadow rays carry path + contribution in the hit record (k_trace_pair)
 #endif
+#ifndef PT_HIT_PATH
+#define PT_HIT_PATH 1  // hit records carry the path id instead of t (shading needs no ray_o read)
+#endif
 #ifndef PT_PAIR_SPECIALISE
 #define PT_PAIR_SPECIALISE 0  // 1: k_trace_pair runs shadow-only waves in an any-hit loop (slower)
 #endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Hit record of a finished extension ray: (t | path, u, v, tri | back << 31), or a miss.
+// The shading kernels reconstruct the surface from (tri, u, v) and never read t, so with
+// PT_HIT_PATH the first word carries the path id and they skip the ray_o read.
+__device__ __forceinline__ float4 hit_record(const Hit& h, int path) {
+    const float x = PT_HIT_PATH ? __int_as_float(path) : h.t;
+    return h.tri >= 0 ? make_float4(x, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
+                      : make_float4(PT_HIT_PATH ? x : 0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+}
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -78,6 +90,18 @@ inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * k
 // starves waves.)
 constexpr int kBlockSh = 1024;
 constexpr int kWavesSh = kBlockSh / 64;
+// k_shade_fused waves per SIMD: a CU holds two 1024-thread blocks only at <= 64 VGPRs (8 waves
+// per SIMD); at 65..128 VGPRs one block per CU halves the occupancy (measured: 66 VGPRs made
+// the Lambert shade 37 % slower).  Lambert fits 64 VGPRs untextured; Dielectric spills ~22
+// VGPRs at 64 and still runs 6 % faster (1,795 -> 1,905 Msamples/s); Conductor spills ~41
+// and is 1.4 % slower, so it keeps its natural allocation.
+#ifndef PT_SHF_WAVES
+#define PT_SHF_WAVES 8
+#endif
+#ifndef PT_SHF_WAVES_OTHER
+#define PT_SHF_WAVES_OTHER 1
+#endif
+constexpr int shf_waves(int mode) { return (mode == 1 || mode == 3) /*Lambert, Dielectric*/ ? PT_SHF_WAVES : PT_SHF_WAVES_OTHER; }
 // k_shade_b (Default / Layered: the stochastic GlossyDiffuse eval + sample) needs more than
 // the 128 VGPRs a 1024-thread block allows, so it runs in smaller blocks.
 #ifndef PT_SHB_BLOCK
@@ -241,13 +265,12 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
         [&](int ri, TravState& st) {
             const float4 a = ldq(ro + ri), c = ldq(rd + ri);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
+            st.path = __float_as_int(a.w);
         },
         [&](int ri, const TravState& st) {
-            const Hit& h = st.h;
-            const float4 rec = h.tri >= 0 ? make_float4(h.t, h.u, h.v,
-                                                        __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                                          : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
-            for (int k = 0; k < dup; ++k) stq(W.hit + ri + (size_t)k * n_trace, rec);
+            // copy k of a bounce-0 ray is path st.path + k * n_trace (queue 0 is in path order)
+            for (int k = 0; k < dup; ++k)
+                stq(W.hit + ri + (size_t)k * n_trace, hit_record(st.h, st.path + k * n_trace));
         });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n);        // path segments
@@ -337,7 +360,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
 }
 
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+__global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
@@ -353,10 +376,11 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch 
         float stmax = 0.0f;
         int path = 0;
         if (valid) {
-            const float4 a = ro[i], c = rd[i];
-            path = __float_as_int(a.w);
-            const Hit h = decode_hit(W.hit[i]);
+            const float4 hv = W.hit[i];
+            path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
+            const Hit h = decode_hit(hv);
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
+                const float4 c = rd[i];
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
@@ -394,7 +418,9 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_fused(DevScene S, DevLaunch 
                     }
                 }
                 BSample bs;
-                if (bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
+                // the last bounce's sampled direction is never traced (SamplePath :646)
+                if ((!PT_SKIP_LAST_SAMPLE || b + 1 < L.max_bounces) &&
+                    bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
                     emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
                     W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
                 }
@@ -432,6 +458,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
             if (i < n_ext) {
                 const float4 a = ldq(ro + i), c = ldq(rd + i);
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
+                st.path = __float_as_int(a.w);
             } else {
                 const int j = i - n_ext;
                 const float4 a = ldq(W.sh_o + j), c = ldq(W.sh_d + j);
@@ -451,9 +478,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
     auto finish = [&](int i, const TravState& st) {
             const Hit& h = st.h;
             if (i < n_ext) {
-                stq(W.hit + i, h.tri >= 0 ? make_float4(h.t, h.u, h.v,
-                                                        __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                                          : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(kMissTri)));
+                stq(W.hit + i, hit_record(h, st.path));
             } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
 #if PT_SHADOW_CARRY
                 const int path = h.orig;
@@ -516,10 +541,11 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
         float stmax = 0.0f;
         int path = 0;
         if (valid) {
-            const float4 a = ro[i], c = rd[i];
-            path = __float_as_int(a.w);
-            const Hit h = decode_hit(W.hit[i]);
+            const float4 hv = W.hit[i];
+            path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
+            const Hit h = decode_hit(hv);
             if (h.tri >= 0) {
+                const float4 c = rd[i];
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
                 float4 bv = W.beta[path];
@@ -615,8 +641,9 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
     const int i = (int)(blockIdx.x * kBlockShB + threadIdx.x);
     bool hit = false, nee = false, conductor = false;
     if (i < n) {
-        const int path = __float_as_int(ro[i].w);
-        hit = __float_as_int(W.hit[i].w) != kMissTri;
+        const float4 hv = W.hit[i];
+        const int path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
+        hit = __float_as_int(hv.w) != kMissTri;
         if (hit) {
             const int aux = W.aux[path];
             conductor = PT_SHB_BUCKET && (aux & 1);
@@ -626,14 +653,16 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
     int n_nee, n_smp;
     const int s_nee = block_bucket_scan<kW>(nee, conductor, lds_scan_a, n_nee);
     if (nee) lds_nee[s_nee] = i;
-    const int s_smp = block_bucket_scan<kW>(hit, conductor, lds_scan_b, n_smp);
-    if (hit) lds_smp[s_smp] = i;
+    // the last bounce's sampled direction is never traced (SamplePath :646): no sample items
+    const bool smp = hit && (!PT_SKIP_LAST_SAMPLE || b + 1 < L.max_bounces);
+    const int s_smp = block_bucket_scan<kW>(smp, conductor, lds_scan_b, n_smp);
+    if (smp) lds_smp[s_smp] = i;
     __syncthreads();
     if ((int)threadIdx.x < n_nee) {  // NEE: the light is visible (devicePrograms.cu:446-472)
         const int j = lds_nee[threadIdx.x];
-        const float4 a = ro[j], c = rd[j];
-        const int path = __float_as_int(a.w);
-        const Hit h = decode_hit(W.hit[j]);
+        const float4 hv = W.hit[j], c = rd[j];
+        const int path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[j].w);
+        const Hit h = decode_hit(hv);
         SurfaceHit sf;
         reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
         const float4 bv = W.beta[path];
@@ -663,9 +692,9 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
     int path = 0;
     if ((int)threadIdx.x < n_smp) {  // BSDF sample + continuation (devicePrograms.cu:474-509)
         const int j = lds_smp[threadIdx.x];
-        const float4 a = ro[j], c = rd[j];
-        path = __float_as_int(a.w);
-        const Hit h = decode_hit(W.hit[j]);
+        const float4 hv = W.hit[j], c = rd[j];
+        path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[j].w);
+        const Hit h = decode_hit(hv);
         d = mk(c.x, c.y, c.z);
         SurfaceHit sf;
         reconstruct<TEX>(S, h, d, sf);
