@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
 // This wave's static slice of a queue of length n (grid sized to residency, so every wave
 // is resident and slices balance statistically; no fetch atomics).
 #ifndef PT_REFILL_MIN
-#define PT_REFILL_MIN 8
+#define PT_REFILL_MIN 24  // idle lanes before a wave refills: each refill stalls the wave for one HBM round trip (sweep: 8 -> 24 = +6.5 %)
 #endif
 constexpr int kRefillMin = PT_REFILL_MIN;
 #ifndef PT_TRI_BATCH
@@ -910,7 +910,9 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         // the table's rays must not be traced again as bounce-0 shadow rays
         return hipMemsetAsync(W.count + kShadowQ * kCntStride, 0, sizeof(int), stream);
     };
-    if (fused) {
+    if (maxb <= 0) {
+        // SamplePath's loop never runs (devicePrograms.cu:646): black frames, no segments
+    } else if (fused) {
         // extend(0); then per bounce: shade(b) -> [shadow rays of b + extension rays of b+1]
         if ((e = extend(0, primary_dedup ? nf : 1)) != hipSuccess) return e;
         if ((e = shadow0()) != hipSuccess) return e;

@@ -317,3 +317,37 @@ def test_textured_scene_parity(variant, kernel):
     assert close_fraction(img, want) >= CLOSE_MIN
     ref, _ = oracle_render(sc, 32, 24, 4, 1, 4)
     np.testing.assert_array_equal(ref, want)
+
+
+@pytest.mark.parametrize("n_lights", [4, 6])
+@pytest.mark.parametrize("depth", [0, 1, 2])
+@pytest.mark.parametrize("mode", [1, 3, 0])
+def test_shallow_depth_and_light_count(depth, mode, n_lights):
+    """Edge cases of the bounce loop (devicePrograms.cu:646): depth 0 renders black, depth 1
+    is a bounce-0-only path whose BSDF sample is skipped (its ray would never be traced),
+    and more lights than frames per batch turns the bounce-0 shadow table off.  Wavefront
+    (batched and not) and megakernel agree bit for bit and match the oracle."""
+    import dataclasses
+
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("diffuse")
+    lights = np.concatenate([sc.lights, sc.lights[:1] * np.array([1, 1, 1, 0.5, 0.5, 0.5], np.float32)])
+    while len(lights) < n_lights:
+        extra = lights[-1:].copy()
+        extra[0, 0] += 0.1 * len(lights)
+        lights = np.concatenate([lights, extra])
+    sc = dataclasses.replace(sc, lights=np.ascontiguousarray(lights[:n_lights], np.float32))
+    wf, sw = gpu_render(sc, 40, 32, depth, 3, 5, mode=mode, kernel=1, frames_per_launch=4)
+    wf1, _ = gpu_render(sc, 40, 32, depth, 3, 5, mode=mode, kernel=1, frames_per_launch=1)
+    mega, sm = gpu_render(sc, 40, 32, depth, 3, 5, mode=mode, kernel=0)
+    np.testing.assert_array_equal(wf, mega)
+    np.testing.assert_array_equal(wf1, mega)
+    assert sw["segments"] == sm["segments"]
+    if depth == 0:
+        assert np.all(wf == 0) and sw["segments"] == 0
+        return
+    o, segs = oracle_render(sc, 40, 32, depth, 3, 5, mode=mode)
+    assert image_mse(wf / 5, o / 5) <= MSE_TOL
+    assert close_fraction(wf, o) >= CLOSE_MIN
+    assert abs(sw["segments"] - segs) <= 0.01 * segs + 2
