@@ -52,6 +52,9 @@ constexpr int kMissTri = -1;
 #ifndef PT_HIT_PATH
 #define PT_HIT_PATH 1  // hit records carry the path id instead of t (shading needs no ray_o read)
 #endif
+#ifndef PT_PAIR_BALANCE
+#define PT_PAIR_BALANCE 0  // 1: each k_trace_pair wave takes a share of both ray kinds (slower)
+#endif
 #ifndef PT_PAIR_SPECIALISE
 #define PT_PAIR_SPECIALISE 0  // 1: k_trace_pair runs shadow-only waves in an any-hit loop (slower)
 #endif
@@ -194,11 +197,16 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 #endif
 }
 
+struct IdentityMap {
+    __device__ int operator()(int v) const { return v; }
+};
+
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
-// for ray ri, `finish(ri, state)` consumes a finished ray.
-template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
+// for ray ri, `finish(ri, state)` consumes a finished ray.  The loop walks positions
+// [next, end); `map` turns a position into the queue index ri.
+template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Map = IdentityMap>
 __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TravStats& ts,
-                                            Fetch fetch, Finish finish) {
+                                            Fetch fetch, Finish finish, Map map = Map()) {
     int spill[kSpillDepth];
     TravState st;
     int ri = -1;
@@ -209,7 +217,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         if (__popcll(m) < kRefillMin && m != ~0ull && next < end) m = 0;
         const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         if (need && m && next + pre < end) {
-            ri = next + pre;
+            ri = map(next + pre);
             fetch(ri, st);
             if (STATS) ts.rays++;
             if (S.ntri <= 0) {  // empty scene: no BVH root, every ray misses
@@ -455,6 +463,9 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
     int* stk = stack + threadIdx.x;
     TravStats ts;
     auto fetch = [&](int i, TravState& st) {
+#ifdef PT_EXP_FAKEFETCH  // timing experiment only: ray records from an L2-resident window (wrong images)
+            i = i < n_ext ? (i % PT_EXP_FAKEFETCH) : n_ext + ((i - n_ext) % PT_EXP_FAKEFETCH);
+#endif
             if (i < n_ext) {
                 const float4 a = ldq(ro + i), c = ldq(rd + i);
                 trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
@@ -492,6 +503,20 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
         };
+#if PT_PAIR_BALANCE
+    // Every wave takes an equal share of BOTH queues (its extension slice, then its shadow
+    // slice): a closest-hit extension ray costs more steps than an any-hit shadow ray, so
+    // contiguous slices of [extension | shadow] would leave the shadow-only waves idle while
+    // the extension waves finish (the grid holds exactly the resident waves).
+    {
+        int e0, e1, s0, s1;
+        wave_slice(n_ext, e0, e1);
+        wave_slice(n_sh, s0, s1);
+        const int ne = e1 - e0;
+        trace_range<kRayMixed, STATS, TEX>(S, 0, ne + (s1 - s0), stk, ts, fetch, finish,
+                                           [=](int v) { return v < ne ? e0 + v : n_ext + s0 + (v - ne); });
+    }
+#else
     // The queue is [extension rays | shadow rays] and wave slices are contiguous, so all but
     // one wave trace a single ray kind: those run a loop specialised to it (no child sort and
     // no closest-hit bookkeeping for shadow rays, no any-hit tests for extension rays).
@@ -508,6 +533,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
     else
 #endif
         trace_range<kRayMixed, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
+#endif
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
