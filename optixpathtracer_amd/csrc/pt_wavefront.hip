@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
 // This wave's static slice of a queue of length n (grid sized to residency, so every wave
 // is resident and slices balance statistically; no fetch atomics).
 #ifndef PT_REFILL_MIN
-#define PT_REFILL_MIN 24  // idle lanes before a wave refills: each refill stalls the wave for one HBM round trip (sweep: 8 -> 24 = +6.5 %)
+#define PT_REFILL_MIN 24  // idle lanes before a wave refills (sweep 8 -> 24: +6.5 %)
 #endif
 constexpr int kRefillMin = PT_REFILL_MIN;
 #ifndef PT_TRI_BATCH
