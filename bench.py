@@ -13,6 +13,9 @@ accumulators are summed to rank 0 with one RCCL reduce (torch.distributed "nccl"
 over xGMI).  Per-GPU work is fixed as N grows ("weak" scaling); value = all samples of
 all ranks / max-over-ranks wall time.
 
+`--config 3|4d|4l|5` runs BASELINE.json's other configs through the same harness (4d/4l split
+4096 spp over the ranks: strong scaling); the driver's default run is configs[1].
+
 Extra fields: `roofline` (HBM roofline of the dominant kernels, the wavefront's trace kernels
 k_extend + k_trace_pair: 48 algorithmic bytes per traced ray, ray read + result write, over
 their per-launch average measured with one HIP event pair per launch on the library stream;
@@ -39,6 +42,23 @@ BYTES_PER_SAMPLE = 12  # final fp32 RGB accumulate
 BYTES_PER_TRACE = 48  # trace-kernel share per ray: ray record read 32 B + hit / result write 16 B
 
 
+# BASELINE.json configs by index: scene, spp per step, scaling, workload label.  The default
+# (configs[1]) is the headline; the others are reported in DESIGN.md from the same harness.
+CONFIGS = {
+    "2": ("sphere_box_diffuse", 1024, "weak",
+          "BASELINE configs[1]: Diffuse sphere-in-box 1920x1080, 1024 spp, depth 8"),
+    "3": ("sphere_box_conductor", 1024, "weak",
+          "BASELINE configs[2]: Conductor (Trowbridge-Reitz) spheres + Layered walls (Default mode), "
+          "1920x1080, 1024 spp, depth 8"),
+    "4d": ("sphere_box_dielectric20", 4096, "strong",
+           "BASELINE configs[3] (i): Dielectric-bright 1920x1080, 4096 spp split over the GPUs + RCCL reduce"),
+    "4l": ("sphere_box_layered", 4096, "strong",
+           "BASELINE configs[3] (ii): Layered 1920x1080, 4096 spp split over the GPUs + RCCL reduce"),
+    "5": ("sponza_class", 1024, "weak",
+          "BASELINE configs[4]: Sponza-class procedural atrium (~250k tris, mixed BRDFs) 1920x1080, 1024 spp"),
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -48,10 +68,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="sphere_box_diffuse")
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
+                    help="BASELINE.json config: 2 = configs[1] (default, the headline), 3, 4d, 4l, 5")
+    ap.add_argument("--scene", default=None, help="override the config's scene")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=1024, help="samples per pixel per GPU per step")
+    ap.add_argument("--spp", type=int, default=None,
+                    help="samples per pixel per step: per GPU (weak configs) or in total (strong configs)")
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--kernel", type=int, default=2, help="0 = megakernel, 1 = wavefront, 2 = auto")
     ap.add_argument("--frames-per-launch", type=int, default=64)
@@ -61,7 +84,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
                     help="PMC traffic per launch measured by tools/profile.sh (optional)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    scene, spp, a.scaling, a.workload = CONFIGS[a.config]
+    a.scene = a.scene or scene
+    a.spp = a.spp or spp
+    return a
 
 
 def cpu_baseline(scene, args, budget_s: float):
@@ -136,7 +163,10 @@ def main():
 
     def step(s: int):
         r.accum_clear()
-        first, n = sharding.frame_range(s, rank, world, args.spp)  # disjoint frame ids per (step, rank)
+        if args.scaling == "strong":  # args.spp frames per step in total, split over the ranks
+            first, n = sharding.split_frames(args.spp, rank, world, base=1 + s * args.spp)
+        else:  # args.spp frames per rank per step; disjoint frame ids per (step, rank)
+            first, n = sharding.frame_range(s, rank, world, args.spp)
         r.render_frames(first, n)
         r.synchronize()
         sharding.reduce_accumulator(accum, dist)  # RCCL over xGMI
@@ -165,7 +195,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    samples_total = args.width * args.height * args.spp * args.steps * world
+    per_step_spp = args.spp if args.scaling == "strong" else args.spp * world
+    samples_total = args.width * args.height * per_step_spp * args.steps
     value = samples_total / elapsed / 1e6
     # Transparency: the same step with every frame's (identical) camera ray traced again
     # instead of once per pixel per batch (pt_set_primary_dedup; bit-identical images).
@@ -186,7 +217,7 @@ def main():
             t = torch.tensor([e1], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             e1 = float(t.item())
-        value_nodedup = args.width * args.height * args.spp * world / e1 / 1e6
+        value_nodedup = args.width * args.height * per_step_spp / e1 / 1e6
         r.set_primary_dedup(True)
     if rank == 0:
         nan_px = int(np.isnan(img).any(axis=-1).sum())
@@ -214,7 +245,7 @@ def main():
         if tj.exists():
             try:
                 tjd = json.loads(tj.read_text())
-                if tjd.get("kernel") == dom:
+                if tjd.get("kernel") == dom and tjd.get("config", "2") == args.config:
                     traffic = tjd.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -227,20 +258,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (procedural sphere-in-box scene; reference glTF assets are not in its repo)",
+            "data": f"synthetic (procedural {args.scene} scene; the reference's glTF assets are not in its repo)",
             "config": {
-                "workload": "BASELINE configs[1]: Diffuse sphere-in-box 1920x1080, 1024 spp, depth 8, 1xMI355X"
-                if world == 1 else f"BASELINE configs[1] per GPU, spp-sharded over {world} GPUs + RCCL reduce",
+                "workload": args.workload + (f", {world}xMI355X" if args.scaling == "strong" or world == 1
+                                             else f" per GPU, spp-sharded over {world} GPUs + RCCL reduce"),
                 "scene": args.scene,
                 "triangles": scene.n_triangles,
                 "width": args.width,
                 "height": args.height,
-                "spp_per_gpu_per_step": args.spp,
+                "spp_per_step": args.spp,
+                "spp_per_gpu_per_step": args.spp if args.scaling == "weak" else round(args.spp / world, 2),
                 "max_depth": args.depth,
-                "material_mode": "lambert" if scene.material_mode == 1 else str(scene.material_mode),
+                "material_mode": {0: "default", 1: "lambert", 2: "conductor", 3: "dielectric",
+                                  4: "layered"}.get(scene.material_mode, str(scene.material_mode)),
                 "kernel": {0: "megakernel", 1: "wavefront", 2: "auto (wavefront)"}[args.kernel],
                 "frames_per_launch": args.frames_per_launch,
                 "parallelism": f"spp-shard x{world}",
@@ -266,7 +299,7 @@ def main():
                 # SURVEY.md §8(d) whole-path figure: (segments*396 + samples*12) / render time
                 "pipeline_gbps": round(alg_bytes / max(kernel_s, 1e-9) / 1e9, 2),
             },
-            "image": {"mean": float(np.nanmean(img) / (args.spp * world)), "nan_pixels": nan_px},
+            "image": {"mean": float(np.nanmean(img) / per_step_spp), "nan_pixels": nan_px},
         }
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline (oracle) ...")

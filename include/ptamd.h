@@ -132,7 +132,8 @@ int pt_set_camera(pt_renderer* r, const float position[3], const float inverse_v
                   const float inverse_projection[16]);
 /* OptixRenderer::SetLights(std::vector<PointLight>*) — OptixRenderer.cpp:670-675 (re-settable). */
 int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count);
-/* OptixRenderer::SetMaxBounces(int) — OptixRenderer.cpp:677-679. */
+/* OptixRenderer::SetMaxBounces(int) — OptixRenderer.cpp:677-679.  0 renders black frames;
+ * a negative count returns PT_ERR_INVALID. */
 int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces);
 int pt_set_material_mode(pt_renderer* r, int32_t material_mode);
 int pt_set_kernel(pt_renderer* r, int32_t kernel);

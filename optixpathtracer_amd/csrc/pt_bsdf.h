@@ -27,8 +27,10 @@ __device__ __forceinline__ void disk_polar(uint32_t& seed, float& px, float& py)
     float u1 = rnd(seed);
     float r = sqrtf(u0);
     float theta = 2.0f * pi * u1;
-    px = r * cosf(theta);
-    py = r * sinf(theta);
+    float st, ct;
+    pt_sincosf(theta, st, ct);  // cosf / sinf (pt_math.h: bit-identical to the oracle)
+    px = r * ct;
+    py = r * st;
 }
 // LambertDiffuse.h:35-55
 __device__ __forceinline__ void disk_concentric(uint32_t& seed, float& dx, float& dy) {
@@ -50,8 +52,10 @@ __device__ __forceinline__ void disk_concentric(uint32_t& seed, float& dx, float
         r = oy;
         theta = PiOver2 - PiOver4 * (ox / oy);
     }
-    dx = r * cosf(theta);
-    dy = r * sinf(theta);
+    float st, ct;
+    pt_sincosf(theta, st, ct);
+    dx = r * ct;
+    dy = r * st;
 }
 
 // ---- spherical geometry: SphericalGeometry.h:8-29 ----------------------------------------
@@ -487,7 +491,7 @@ __device__ __forceinline__ float power_heuristic(float fpdf, float gpdf) {  // :
 }
 __device__ __forceinline__ float transmittance(float dz, f3 w) {  // :97-105
     if (gabs(dz) <= 1.17549435e-38f) return 1.0f;
-    return expf(-gabs(dz / w.z));
+    return pt_expf_neg(-gabs(dz / w.z));  // expf (pt_math.h)
 }
 __device__ __forceinline__ f3 layer_f(bool top, f3 albedo, float roughness, f3 wo, f3 wi, int mode) {
     if (top) {

@@ -59,6 +59,7 @@ struct EventPool {
         used++;
         return hipSuccess;
     }
+    void give_back(size_t k) { used -= std::min(k, used); }  // the last k pairs went unrecorded
     hipError_t collect(double* ms_sum, size_t* n) {
         *ms_sum = 0.0;
         *n = used;
@@ -233,10 +234,12 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
                 tev = r->tev_frame.data();
             }
             PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
+            int n_timed = 0;
             PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, nf,
                                           r->primary_dedup, dev_cus,
-                                          r->stream, tev),
+                                          r->stream, tev, &n_timed),
                    "wavefront launch");
+            if (tev) r->tev.give_back((size_t)(r->max_bounces + 1 - n_timed));  // pairs never recorded
             PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
             f += (uint32_t)nf;
         }
@@ -545,6 +548,9 @@ int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count) {
 
 int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_max_bounces: NULL");
+    // SetMaxBounces (OptixRenderer.cpp:677-679) takes any int; a negative count would never
+    // enter SamplePath's loop, like 0, so it is rejected here rather than silently renamed
+    if (max_bounces < 0) return fail(PT_ERR_INVALID, "pt_set_max_bounces: negative count");
     r->max_bounces = max_bounces;
     return PT_OK;
 }

@@ -153,7 +153,7 @@ constexpr int kSpillDepth = PT_SPILL_DEPTH;  // spill + LDS hold a BVH4 path of 
 __device__ __forceinline__ float srgb_to_linear(float c) {
     const float m = (c < 0.04045f) ? 0.0f : 1.0f;  // glm::step
     const float a = c / 12.92f;
-    const float b = powf((c + 0.055f) / 1.055f, 2.4f);  // SavePow
+    const float b = pt_powf_unit((c + 0.055f) / 1.055f, 2.4f);  // SavePow (powf, pt_math.h)
     return a * (1.0f - m) + b * m;                      // SaveMix
 }
 __device__ __forceinline__ int wrapi(int i, int n) {

@@ -56,12 +56,14 @@ size_t wavefront_bytes(int paths, int max_bounces);
 hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces);
 void wavefront_free(WFState& W);
 // Enqueue one frame (all bounces) of the wavefront pipeline; adds the frame into L.accum.
-// trace_events (optional): 2 * L.max_bounces events recorded around each k_extend launch.
+// trace_events (optional): up to 2 * (L.max_bounces + 1) events recorded around the trace
+// launches; *n_timed (optional) receives the number of event pairs recorded.
 // nf frames (frame .. frame + nf - 1) are traced together; W must hold nf * W * H paths.
 // primary_dedup: trace the batch's identical camera rays once per pixel (k_extend `dup`).
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
-                                  const hipEvent_t* trace_events);
+                                  const hipEvent_t* trace_events,
+                                  int* n_timed = nullptr);
 
 // Render launches.
 hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,

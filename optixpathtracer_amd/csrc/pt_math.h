@@ -85,6 +85,67 @@ PT_HD float rnd(uint32_t& prev) {
     prev = 1664525u * prev + 1013904223u;
     return (float)(prev & 0x00FFFFFFu) / (float)0x01000000;
 }
+// ---- transcendentals of the hot path, identical bit for bit to the oracle's -------------
+// The reference calls CUDA libdevice sinf/cosf (random.h:76-84, LambertDiffuse.h:35-55), expf
+// (GlossyDiffuse.h:97-105) and powf (devicePrograms.cu:62-73), whose ulp-level results neither
+// ocml nor glibc reproduce.  The kernels and the CPU oracle (oracle/pt_oracle.c) therefore both
+// evaluate these fixed, explicitly fused single-precision polynomials (Cody-Waite reduction +
+// Cephes minimax coefficients: sin/cos/exp <= ~1 ulp) on the bounded domains the path uses, so GPU and
+// oracle images agree bit for bit instead of diverging on a flipped random decision.
+// sin/cos for |x| <= 2^15 (the path passes |x| <= 2 pi): quadrant k = rint(x * 2/pi), r = x - k pi/2
+// in three fma steps, then sin(r) / cos(r) on [-pi/4, pi/4].
+PT_HD void pt_sincosf(float x, float& s, float& c) {
+    const float k = rintf(x * 0x1.45f306p-1f);
+    float r = fmaf(-k, 0x1.921fb6p+0f, x);
+    r = fmaf(-k, -0x1.777a5cp-25f, r);
+    r = fmaf(-k, -0x1.ee59dap-50f, r);
+    const float z = r * r;
+    const float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+    const float cp = fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
+                          z * z, fmaf(-0.5f, z, 1.0f));
+    const int q = (int)k & 3;
+    s = q == 0 ? sp : q == 1 ? cp : q == 2 ? -sp : -cp;
+    c = q == 0 ? cp : q == 1 ? -sp : q == 2 ? -cp : sp;
+}
+// exp(x) for x <= 0 (transmittance): 0 below -86 (keeps every result a normal float); NaN stays NaN.
+PT_HD float pt_expf_neg(float x) {
+    if (!(x > -86.0f)) return x != x ? x : 0.0f;
+    const float k = floorf(fmaf(x, 0x1.715476p+0f, 0.5f));
+    float r = fmaf(-k, 0.693359375f, x);
+    r = fmaf(-k, -2.12194440e-4f, r);
+    float p = fmaf(fmaf(fmaf(fmaf(fmaf(1.9875691500e-4f, r, 1.3981999507e-3f), r, 8.3334519073e-3f), r,
+                             4.1665795894e-2f), r, 1.6666665459e-1f), r, 5.0000001201e-1f);
+    p = fmaf(p, r * r, r) + 1.0f;
+    return ldexpf(p, (int)k);
+}
+// ln(x) for normal x in (0, 1]: x = m 2^e with m in [sqrt(1/2), sqrt(2)), Cephes logf polynomial.
+PT_HD float pt_logf_unit(float x) {
+    int e;
+    float m = frexpf(x, &e);
+    if (m < 0.70710678118654752f) {
+        m = m + m;
+        e -= 1;
+    }
+    const float f = m - 1.0f, z = f * f;
+    float y = 7.0376836292e-2f;
+    y = fmaf(y, f, -1.1514610310e-1f);
+    y = fmaf(y, f, 1.1676998740e-1f);
+    y = fmaf(y, f, -1.2420140846e-1f);
+    y = fmaf(y, f, 1.4249322787e-1f);
+    y = fmaf(y, f, -1.6668057665e-1f);
+    y = fmaf(y, f, 2.0000714765e-1f);
+    y = fmaf(y, f, -2.4999993993e-1f);
+    y = fmaf(y, f, 3.3333331174e-1f);
+    y = (y * f) * z;
+    const float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(-0.5f, z, y);
+    return (f + y) + fe * 0.693359375f;
+}
+// x^e for x in (0, 1] and e > 0 (the sRGB decode: x >= 0.052, e = 2.4); single-precision
+// exp(e ln x) amplifies the rounding of ln x by e: <= ~7 ulp, immaterial for 8-bit texels
+PT_HD float pt_powf_unit(float x, float e) { return pt_expf_neg(e * pt_logf_unit(x)); }
+
 // PTX cvt.rzi.u32.f32 semantics (saturate, NaN -> 0) for PBRT/GlossyDiffuse.h:215-218,417-418.
 PT_HD uint32_t f2u_sat(float f) {
     if (!(f > 0.0f)) return 0u;

@@ -858,7 +858,7 @@ void wavefront_free(WFState& W) {
 
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
-                                  const hipEvent_t* trace_events) {
+                                  const hipEvent_t* trace_events, int* n_timed) {
     const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
@@ -958,6 +958,7 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         }
     }
     hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
+    if (n_timed) *n_timed = timed;  // fused modes: max_bounces + 1; Default / Layered: max_bounces
     return hipGetLastError();
 }
 

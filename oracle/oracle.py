@@ -62,6 +62,15 @@ BSDF = {"lambert": 0, "conductor": 1, "dielectric": 2, "layered": 3}
 _lib = None
 
 
+def math_eval(fn: str, x) -> np.ndarray:
+    """The oracle's (and the kernels') sin / cos / exp / pow2.4 polynomials on float32 inputs."""
+    lib = load()
+    xs = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(xs)
+    lib.orc_math_eval({"sin": 0, "cos": 1, "exp": 2, "pow2.4": 3}[fn], fp(xs), fp(out), xs.size)
+    return out
+
+
 def build() -> Path:
     subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB
@@ -77,6 +86,7 @@ def load() -> C.CDLL:
     lib.orc_tea16.restype = C.c_uint32
     lib.orc_tea16.argtypes = [C.c_uint32, C.c_uint32]
     lib.orc_rnd_seq.argtypes = [C.c_uint32, C.c_int32, _FP, _UP]
+    lib.orc_math_eval.argtypes = [C.c_int32, _FP, _FP, C.c_int32]
     lib.orc_f2u_sat.restype = C.c_uint32
     lib.orc_f2u_sat.argtypes = [C.c_float]
     lib.orc_bsdf_sample.restype = C.c_int32

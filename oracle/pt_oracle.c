@@ -102,6 +102,69 @@ uint32_t orc_f2u_sat(float f) {
     if (f >= 4294967296.0f) return 0xFFFFFFFFu;
     return (uint32_t)f;
 }
+/* Transcendentals.  The reference calls CUDA libdevice sinf/cosf/expf/powf, whose ulp-level
+ * results glibc does not reproduce (nor does the GPU build's ocml).  The oracle and the HIP
+ * kernels (optixpathtracer_amd/csrc/pt_math.h) both evaluate these fixed, explicitly fused
+ * single-precision polynomials on the bounded domains the path uses (Cody-Waite reduction +
+ * Cephes minimax coefficients: sin/cos/exp within ~1 ulp, x^2.4 within ~7), restated independently so
+ * GPU and oracle agree bit for bit.  fmaf is correctly rounded on both sides. */
+static void orc_sincosf(float x, float* s, float* c) {  /* |x| <= 2^15 */
+    const float k = rintf(x * 0x1.45f306p-1f);
+    float r = fmaf(-k, 0x1.921fb6p+0f, x);
+    r = fmaf(-k, -0x1.777a5cp-25f, r);
+    r = fmaf(-k, -0x1.ee59dap-50f, r);
+    const float z = r * r;
+    const float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+    const float cp = fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
+                          z * z, fmaf(-0.5f, z, 1.0f));
+    const int q = (int)k & 3;
+    *s = q == 0 ? sp : q == 1 ? cp : q == 2 ? -sp : -cp;
+    *c = q == 0 ? cp : q == 1 ? -sp : q == 2 ? -cp : sp;
+}
+static float orc_expf_neg(float x) {  /* x <= 0; 0 below -86, NaN stays NaN */
+    if (!(x > -86.0f)) return x != x ? x : 0.0f;
+    const float k = floorf(fmaf(x, 0x1.715476p+0f, 0.5f));
+    float r = fmaf(-k, 0.693359375f, x);
+    r = fmaf(-k, -2.12194440e-4f, r);
+    float p = fmaf(fmaf(fmaf(fmaf(fmaf(1.9875691500e-4f, r, 1.3981999507e-3f), r, 8.3334519073e-3f), r,
+                             4.1665795894e-2f), r, 1.6666665459e-1f), r, 5.0000001201e-1f);
+    p = fmaf(p, r * r, r) + 1.0f;
+    return ldexpf(p, (int)k);
+}
+static float orc_logf_unit(float x) {  /* normal x in (0, 1] */
+    int e;
+    float m = frexpf(x, &e);
+    if (m < 0.70710678118654752f) { m = m + m; e -= 1; }
+    const float f = m - 1.0f, z = f * f;
+    float y = 7.0376836292e-2f;
+    y = fmaf(y, f, -1.1514610310e-1f);
+    y = fmaf(y, f, 1.1676998740e-1f);
+    y = fmaf(y, f, -1.2420140846e-1f);
+    y = fmaf(y, f, 1.4249322787e-1f);
+    y = fmaf(y, f, -1.6668057665e-1f);
+    y = fmaf(y, f, 2.0000714765e-1f);
+    y = fmaf(y, f, -2.4999993993e-1f);
+    y = fmaf(y, f, 3.3333331174e-1f);
+    y = (y * f) * z;
+    const float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(-0.5f, z, y);
+    return (f + y) + fe * 0.693359375f;
+}
+static float orc_powf_unit(float x, float e) { return orc_expf_neg(e * orc_logf_unit(x)); }
+/* exported for the tests (accuracy against numpy float64) */
+void orc_math_eval(int32_t fn, const float* x, float* out, int32_t n) {
+    for (int32_t i = 0; i < n; ++i) {
+        float s, c;
+        switch (fn) {
+            case 0: orc_sincosf(x[i], &s, &c); out[i] = s; break;
+            case 1: orc_sincosf(x[i], &s, &c); out[i] = c; break;
+            case 2: out[i] = orc_expf_neg(x[i]); break;
+            default: out[i] = orc_powf_unit(x[i], 2.4f); break;
+        }
+    }
+}
+
 /* random.h:76-84; argument evaluation left-to-right (confirmed in devicePrograms.cu.ptx) */
 static void disk_polar(uint32_t* seed, float* px, float* py) {
     const float pi = (float)3.14159265359;
@@ -109,8 +172,10 @@ static void disk_polar(uint32_t* seed, float* px, float* py) {
     float u1 = rnd(seed);
     float r = sqrtf(u0);
     float theta = 2.0f * pi * u1;
-    *px = r * cosf(theta);
-    *py = r * sinf(theta);
+    float st, ct;
+    orc_sincosf(theta, &st, &ct);
+    *px = r * ct;
+    *py = r * st;
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -287,8 +352,10 @@ static void disk_concentric(uint32_t* seed, float* dx, float* dy) {  /* :35-55 *
     float theta, r;
     if (gabs(ox) > gabs(oy)) { r = ox; theta = PiOver4 * (oy / ox); }
     else { r = oy; theta = PiOver2 - PiOver4 * (ox / oy); }
-    *dx = r * cosf(theta);
-    *dy = r * sinf(theta);
+    float st, ct;
+    orc_sincosf(theta, &st, &ct);
+    *dx = r * ct;
+    *dy = r * st;
 }
 static v3 lambert_f(v3 albedo, v3 wo, v3 wi) {  /* :86-92 */
     if (!samehemi(wo, wi)) return mk(0, 0, 0);
@@ -473,7 +540,7 @@ static float power_heuristic(float fpdf, float gpdf) {  /* :91-95 with nf = ng =
 }
 static float transmittance(float dz, v3 w) {  /* :97-105 */
     if (gabs(dz) <= FLT_MIN) return 1.0f;
-    return expf(-gabs(dz / w.z));
+    return orc_expf_neg(-gabs(dz / w.z));
 }
 static v3 layer_f(int top, v3 albedo, float roughness, v3 wo, v3 wi, int mode) {
     return top ? dielectric_f(roughness, wo, wi, mode) : lambert_f(albedo, wo, wi);
@@ -865,7 +932,7 @@ static inline float srgb_to_linear(float c) {
     float m = (c < 0.04045f) ? 0.0f : 1.0f;  /* glm::step(0.04045, c) */
     float a = c / 12.92f;
     float nom = c + 0.055f;
-    float b = powf(nom / 1.055f, 2.4f);       /* SavePow */
+    float b = orc_powf_unit(nom / 1.055f, 2.4f);  /* SavePow */
     return a * (1.0f - m) + b * m;            /* SaveMix */
 }
 static inline int wrapi(int i, int n) { int r = i % n; return r < 0 ? r + n : r; }

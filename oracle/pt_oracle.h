@@ -68,6 +68,9 @@ typedef struct orc_scene orc_scene;
 
 /* --- RNG (random.h:34-69) --- */
 uint32_t orc_tea16(uint32_t v0, uint32_t v1);
+/* The path's transcendentals (shared fixed polynomials, see pt_oracle.c): fn 0 = sin, 1 = cos
+ * (|x| <= 2^15), 2 = exp (x <= 0), 3 = x^2.4 (x in (0, 1]). */
+void orc_math_eval(int32_t fn, const float* x, float* out, int32_t n);
 void orc_rnd_seq(uint32_t seed, int32_t n, float* out, uint32_t* seed_out);
 uint32_t orc_f2u_sat(float f);
 

@@ -245,3 +245,31 @@ def test_golden_textured_images(oracle_lib, golden):
         base, _ = plain.render(plain.launch(32, 24, 4), 1, 4, threads=3)
         plain.close()
         assert np.abs(img - base).mean() > 1e-3
+
+
+def test_path_transcendentals_accuracy(oracle_lib):
+    """sin / cos / exp / pow2.4 of the path (pt_oracle.c, restated in pt_math.h for the
+    kernels): a fixed fused polynomial on both sides so GPU and oracle agree bit for bit; it
+    must stay within a few ulp of the true function, like the libdevice calls it replaces."""
+    rng = np.random.default_rng(7)
+    x = np.concatenate([np.linspace(-8, 8, 20001), rng.uniform(-2 * np.pi, 2 * np.pi, 20000),
+                        np.array([0.0, -0.0, np.pi / 4, np.pi / 2, np.pi, 2 * np.pi])]).astype(np.float32)
+    x64 = x.astype(np.float64)
+    for fn, ref in (("sin", np.sin), ("cos", np.cos)):
+        got = oracle_lib.math_eval(fn, x).astype(np.float64)
+        err = np.abs(got - ref(x64))
+        assert err.max() <= 2.5e-7, (fn, err.max())  # |value| <= 1: a few ulp of 1
+    xe = np.concatenate([np.linspace(-85.9, 0, 20001), -rng.exponential(2.0, 20000)]).astype(np.float32)
+    xe = xe[xe > -86]
+    got = oracle_lib.math_eval("exp", xe).astype(np.float64)
+    rel = np.abs(got - np.exp(xe.astype(np.float64))) / np.exp(xe.astype(np.float64))
+    assert rel.max() <= 3.6e-7, rel.max()
+    assert oracle_lib.math_eval("exp", np.array([-90.0, -np.inf], np.float32)).tolist() == [0.0, 0.0]
+    assert np.isnan(oracle_lib.math_eval("exp", np.array([np.nan], np.float32))[0])
+    assert oracle_lib.math_eval("exp", np.array([0.0], np.float32))[0] == 1.0
+    xp = np.linspace(0.05, 1.0, 20001).astype(np.float32)
+    got = oracle_lib.math_eval("pow2.4", xp).astype(np.float64)
+    want = xp.astype(np.float64) ** 2.4
+    # exp(2.4 * ln x) in single precision: the rounding of ln x is amplified 2.4x (<= ~7 ulp),
+    # immaterial for decoding 8-bit texels
+    assert (np.abs(got - want) / want).max() <= 1e-6
