@@ -151,6 +151,33 @@ int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
  * bit-identical either way. */
 int pt_set_primary_dedup(pt_renderer* r, int32_t enable);
 
+/* LaunchParams (Renderer/OptiX/LaunchParams.h:9-28) as a C struct: the state one optixLaunch
+ * reads.  Same fields and meaning; device pointers where the reference holds device pointers
+ * (colorBuffer and pointlights are CUDABuffer d_pointer()s, OptixRenderer.cpp:617-637,670-675);
+ * `traversable` is replaced by the renderer's own BVH. */
+typedef struct pt_launch_params {
+    struct {
+        float* color_buffer; /* device: size[0]*size[1] glm::vec3 (RGB fp32), row 0 = bottom */
+        int32_t size[2];
+        uint32_t id; /* seeds tea<16>(W*y+x, id) (devicePrograms.cu:631) */
+    } frame;
+    struct {
+        float position[3];
+        float inverse_view_matrix[16];       /* column-major (glm) */
+        float inverse_projection_matrix[16]; /* column-major (glm) */
+    } camera;
+    const pt_point_light* point_lights; /* device array of point_light_count lights */
+    int32_t point_light_count;
+    int32_t max_bounces;
+} pt_launch_params;
+
+/* optixLaunch(pipeline, stream, launchParams, ..., size.x, size.y, 1) — OptixRenderer.cpp:627-637
+ * running __raygen__renderFrame (devicePrograms.cu:666-706): every pixel's sample of frame.id is
+ * written (not added) to frame.color_buffer.  Asynchronous on pt_stream(r); pt_synchronize waits
+ * (the reference's CUDA_SYNC_CHECK).  The renderer's own size, camera, lights and max bounces are
+ * not changed.  A zero size is a no-op; a negative max_bounces or count is PT_ERR_INVALID. */
+int pt_launch(pt_renderer* r, const pt_launch_params* params);
+
 /* OptixRenderer::Render(glm::vec3 h_pixels[]) — OptixRenderer.cpp:617-647: frame.id++,
  * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before
  * the first pt_resize (as :621). */

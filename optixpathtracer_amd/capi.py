@@ -100,6 +100,21 @@ class pt_stats(C.Structure):
     ]
 
 
+class _pt_launch_frame(C.Structure):
+    _fields_ = [("color_buffer", C.c_void_p), ("size", C.c_int32 * 2), ("id", C.c_uint32)]
+
+
+class _pt_launch_camera(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("inverse_view_matrix", C.c_float * 16),
+                ("inverse_projection_matrix", C.c_float * 16)]
+
+
+class pt_launch_params(C.Structure):
+    """LaunchParams (Renderer/OptiX/LaunchParams.h:9-28); device pointers as in the reference."""
+    _fields_ = [("frame", _pt_launch_frame), ("camera", _pt_launch_camera), ("point_lights", C.c_void_p),
+                ("point_light_count", C.c_int32), ("max_bounces", C.c_int32)]
+
+
 _FP = C.POINTER(C.c_float)
 _IP = C.POINTER(C.c_int32)
 _R = C.c_void_p  # pt_renderer*
@@ -122,6 +137,7 @@ SIGNATURES = {
     "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel_timing": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),
+    "pt_launch": (C.c_int, [_R, C.POINTER(pt_launch_params)]),
     "pt_accum_clear": (C.c_int, [_R]),
     "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),
     "pt_set_primary_dedup": (C.c_int, [_R, C.c_int32]),

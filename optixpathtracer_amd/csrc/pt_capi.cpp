@@ -583,6 +583,46 @@ int pt_render(pt_renderer* r, float* host_rgb) {
     return collect_pending(r);
 }
 
+int pt_launch(pt_renderer* r, const pt_launch_params* lp) {
+    static_assert(sizeof(pt_point_light) == sizeof(DevLight), "pt_point_light is read as DevLight on the device");
+    if (!r || !lp) return fail(PT_ERR_INVALID, "pt_launch: NULL");
+    const int w = lp->frame.size[0], h = lp->frame.size[1];
+    if (w < 0 || h < 0 || lp->point_light_count < 0 || lp->max_bounces < 0)
+        return fail(PT_ERR_INVALID, "pt_launch: negative size, light count or max bounces");
+    if (w == 0 || h == 0) return PT_OK;  // an empty launch grid
+    if (!lp->frame.color_buffer || (lp->point_light_count > 0 && !lp->point_lights))
+        return fail(PT_ERR_INVALID, "pt_launch: NULL color buffer or lights");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    // this launch's state replaces the renderer's for the duration of the enqueue only
+    const int ow = r->width, oh = r->height, on = r->n_lights, ob = r->max_bounces;
+    float opos[3], oview[16], oproj[16];
+    std::memcpy(opos, r->cam_pos, sizeof opos);
+    std::memcpy(oview, r->inv_view, sizeof oview);
+    std::memcpy(oproj, r->inv_proj, sizeof oproj);
+    DevLight* olights = r->d_lights;
+    r->width = w;
+    r->height = h;
+    std::memcpy(r->cam_pos, lp->camera.position, sizeof r->cam_pos);
+    std::memcpy(r->inv_view, lp->camera.inverse_view_matrix, sizeof r->inv_view);
+    std::memcpy(r->inv_proj, lp->camera.inverse_projection_matrix, sizeof r->inv_proj);
+    r->d_lights = reinterpret_cast<DevLight*>(const_cast<pt_point_light*>(lp->point_lights));
+    r->n_lights = lp->point_light_count;
+    r->max_bounces = lp->max_bounces;
+    // colorBuffer[fbIndex] = pathRadiance (devicePrograms.cu:705): a one-frame sum into zeros
+    hipError_t e = hipMemsetAsync(lp->frame.color_buffer, 0, sizeof(float) * 3 * (size_t)w * (size_t)h, r->stream);
+    int rc = e == hipSuccess ? launch_frames(r, lp->frame.color_buffer, lp->frame.id, 1)
+                             : fail(PT_ERR_HIP, std::string("pt_launch: hipMemsetAsync: ") + hipGetErrorString(e));
+    r->width = ow;
+    r->height = oh;
+    std::memcpy(r->cam_pos, opos, sizeof opos);
+    std::memcpy(r->inv_view, oview, sizeof oview);
+    std::memcpy(r->inv_proj, oproj, sizeof oproj);
+    r->d_lights = olights;
+    r->n_lights = on;
+    r->max_bounces = ob;
+    return rc;
+}
+
 int pt_display_reset(pt_renderer* r, int32_t max_samples) {
     if (!r) return fail(PT_ERR_INVALID, "pt_display_reset: NULL");
     if (r->width == 0) return fail(PT_ERR_STATE, "pt_display_reset: call pt_resize first");

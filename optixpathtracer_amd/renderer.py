@@ -116,6 +116,25 @@ class OptixRenderer:
         check(self.lib.pt_render(self.h, fptr(out)), "pt_render")
         return out
 
+    def launch(self, color_buffer_ptr: int, size, frame_id: int, position, inverse_view, inverse_projection,
+               lights_device_ptr: int, n_lights: int, max_bounces: int) -> None:
+        """optixLaunch with a LaunchParams block (pt_launch): writes frame `frame_id`'s 1-spp
+        radiance into the device buffer at color_buffer_ptr (W*H*3 fp32, row 0 = bottom).
+        Asynchronous; call synchronize().  Device pointers, as in the reference."""
+        lp = capi.pt_launch_params()
+        lp.frame.color_buffer = C.c_void_p(int(color_buffer_ptr))
+        lp.frame.size[0], lp.frame.size[1] = int(size[0]), int(size[1])
+        lp.frame.id = int(frame_id)
+        for dst, src in ((lp.camera.position, position), (lp.camera.inverse_view_matrix, inverse_view),
+                         (lp.camera.inverse_projection_matrix, inverse_projection)):
+            vals = _f32(src).ravel()
+            for i, v in enumerate(vals):
+                dst[i] = float(v)
+        lp.point_lights = C.c_void_p(int(lights_device_ptr)) if lights_device_ptr else None
+        lp.point_light_count = int(n_lights)
+        lp.max_bounces = int(max_bounces)
+        check(self.lib.pt_launch(self.h, C.byref(lp)), "pt_launch")
+
     def SetCamera(self, position, inverse_view, inverse_projection) -> None:  # :662-668
         check(self.lib.pt_set_camera(self.h, fptr(_f32(position)), fptr(_f32(inverse_view)),
                                      fptr(_f32(inverse_projection))), "pt_set_camera")
