@@ -140,6 +140,9 @@ constexpr int kSpillDepth = PT_SPILL_DEPTH;  // spill + LDS hold a BVH4 path of 
 #ifndef PT_TRI_PER_STEP
 #define PT_TRI_PER_STEP 1
 #endif
+#ifndef PT_TRIS_PER_DUAL
+#define PT_TRIS_PER_DUAL 1  // triangles a dual step may test from its leaf
+#endif
 #ifndef PT_SKIP_LAST_SAMPLE
 #define PT_SKIP_LAST_SAMPLE 1  // no BSDF sample on a path's last segment (its ray is never traced)
 #endif
@@ -583,6 +586,9 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
 #else
     if (tri_ok && s.leaf != kEmptyChild) {
         if (leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
+#if PT_TRIS_PER_DUAL > 1
+        if (s.leaf != kEmptyChild && leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
+#endif
     }
     if (s.cur >= 0) {
         if (STATS) ts.nodes++;
