@@ -256,6 +256,9 @@ __device__ __forceinline__ float lambert_pdf(f3 wo, f3 wi, bool reflection) {
 }
 
 // ---- Dielectric (eta = 1.5): Dielectric.h:20-343 -------------------------------------------
+#ifndef PT_DIEL_CONVERGED
+#define PT_DIEL_CONVERGED 1  // rough dielectric sample: both lobes' shared terms computed once
+#endif
 enum { kRadiance = 0, kImportance = 1 };
 __device__ __forceinline__ float fresnel_dielectric(float cos_i, float ior) {  // :20-42
     cos_i = gclamp(cos_i, -1.0f, 1.0f);
@@ -356,6 +359,41 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
     if (!reflection) pr = 0.0f;
     if (!transmission) pt = 0.0f;
     if (pr == 0.0f && pt == 0.0f) return false;
+#if PT_DIEL_CONVERGED
+    // The reflection and transmission branches (:162-236) run in the same wave whenever its
+    // lanes draw different lobes (nearly always: R is a few percent).  Both branches evaluate
+    // D(wm) and Lambda(wi) and end in the same divisions, so they are computed once here, on the
+    // lane's own wi and with each division's operands selected per lobe: every value is the one
+    // its branch computes, with one copy of the expensive terms instead of two.
+    const bool refl = uc < pr / (pr + pt);
+    const f3 I = -wo;  // glm::reflect(I, N) = I - N*dot(N,I)*2
+    const float dr = dot(wm, I);
+    const f3 wr = mk(I.x - wm.x * dr * 2.0f, I.y - wm.y * dr * 2.0f, I.z - wm.z * dr * 2.0f);
+    float etap_t = 1.0f;
+    f3 wt = mk(0, 0, 0);
+    const bool tir = !refract(wo, wm, eta, etap_t, wt);
+    const f3 wi = refl ? wr : wt;
+    if (refl ? !same_hemisphere(wo, wi) : (tir || same_hemisphere(wo, wi) || wi.z == 0.0f)) return false;
+    const float etap = refl ? 1.0f : etap_t;
+    const float D = tr_D(wm, alpha);
+    const float G = 1.0f / (1.0f + p.lam + tr_lambda(wi, alpha));
+    const float adw = abs_dot(wo, wm);
+    const float A = p.g1c * D * adw;
+    const float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);            // transmission only
+    const float q1 = (refl ? A : abs_dot(wi, wm)) / (refl ? 4.0f * adw : denom);  // A/(4|wo.wm|) | dwm_dwi
+    const float pdf = (refl ? q1 * pr : A * q1 * pt) / (pr + pt);
+    const float q2 = (refl ? D * G * R : dot(wi, wm) * dot(wo, wm)) / (refl ? 4.0f * wi.z * wo.z : wi.z * wo.z * denom);
+    float f = refl ? q2 : T * D * G * fabsf(q2);
+    const float fd = f / sqr(etap);
+    if (!refl && mode == kRadiance) f = fd;
+    s.color = mk(f, f, f);
+    s.dir = wi;
+    s.pdf = pdf;
+    s.refl = refl;
+    s.trans = !refl;
+    s.spec = false;
+    return true;
+#else
     if (uc < pr / (pr + pt)) {
         f3 I = -wo;  // glm::reflect(I, N) = I - N*dot(N,I)*2
         float d = dot(wm, I);
@@ -387,6 +425,7 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
     s.trans = true;
     s.spec = false;
     return true;
+#endif
 }
 __device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughness, f3 wo, BSample& s,
                                                   int mode, bool reflection, bool transmission) {
@@ -453,6 +492,22 @@ __device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, con
     const float G = 1.0f / (1.0f + po.lam + lam_i);
     const float tp = po.g1c * D * abs_dot(wo, wm);
     float fv, pv;
+#if PT_DIEL_CONVERGED
+    // reflection and transmission in one sequence (lanes of a wave disagree on `reflect`): each
+    // division takes its lobe's operands, so every value equals its branch's below
+    const float R = F, T = 1.0f - R;
+    float pr = R, pt = T;
+    if (!reflection) pr = 0.0f;
+    if (!transmission) pt = 0.0f;
+    const float s2 = sqr(dot(wi, wm) + dot(wo, wm) / etap);  // transmission only
+    const float qf = (reflect ? D * G * F : dot(wi, wm) * dot(wo, wm)) / (reflect ? fabsf(4.0f * ci * co) : s2 * ci * co);
+    fv = reflect ? qf : D * (1.0f - F) * G * fabsf(qf);
+    const float fd = fv / sqr(etap);
+    if (!reflect && mode == kRadiance) fv = fd;
+    const float qp = (reflect ? tp : abs_dot(wi, wm)) / (reflect ? 4.0f * abs_dot(wo, wm) : s2);
+    pv = (reflect ? qp * pr : tp * qp * pt) / (pr + pt);
+    if (pr == 0.0f && pt == 0.0f) pv = 0.0f;
+#else
     if (reflect) {
         fv = D * G * F / fabsf(4.0f * ci * co);
     } else {
@@ -473,6 +528,7 @@ __device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, con
         float dwm_dwi = abs_dot(wi, wm) / denom;
         pv = tp * dwm_dwi * pt / (pr + pt);
     }
+#endif
     f = f_ok ? fv : 0.0f;
     pdf = p_ok ? pv : 0.0f;
 }
