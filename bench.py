@@ -312,6 +312,8 @@ def main():
             gpu = accum.cpu().numpy()[args.height - band.shape[0]:].astype(np.float64) / spp_cpu
             ref = band.astype(np.float64) / spp_cpu
             diff = np.nan_to_num(gpu, nan=0.0) - np.nan_to_num(ref, nan=0.0)  # NaN -> 0 (WriteImage.cpp:52-55)
+            if os.environ.get("PT_BENCH_DUMP"):  # debug aid: both band sums for offline comparison
+                np.savez(os.environ["PT_BENCH_DUMP"], gpu=accum.cpu().numpy()[args.height - band.shape[0]:], ref=band)
             out["mse_vs_oracle"] = {
                 "mse": float(np.mean(diff * diff)),
                 "max_abs": float(np.max(np.abs(diff))),
