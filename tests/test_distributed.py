@@ -87,3 +87,52 @@ def test_shard_ranges_partition_the_frames():
             assert not (s & seen)
             seen |= s
     assert seen == set(range(1, 1 + 3 * 4 * 16))
+
+
+def _gpu_worker(rank, world, port, total_spp, out_dir):
+    sys.path.insert(0, str(ROOT))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from optixpathtracer_amd import scenes, sharding
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = scenes.tiny_scene("conductor")
+    r = setup_renderer(sc, 48, 32, 5, device=0)
+    r.set_frames_per_launch(4)
+    r.accum_clear()
+    first, n = sharding.split_frames(total_spp, rank, world)
+    r.render_frames(first, n)
+    t = torch.from_numpy(r.accum())
+    r.close()
+    sharding.reduce_accumulator(t, dist)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "gpu_strong.npy"), t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_process_gpu_shards_reduce_to_single_render(tmp_path):
+    """The bench's multi-GPU path with two processes on one card: each renders its frame-id
+    shard through libptamd, the host accumulators are summed over gloo (RCCL needs one GPU
+    per rank), and the result equals one process rendering every frame, up to the fp32
+    order of the cross-rank sum."""
+    import torch.multiprocessing as mp
+
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    world, spp = 2, 11
+    mp.spawn(_gpu_worker, args=(world, _free_port(), spp, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(tmp_path / "gpu_strong.npy")
+    sc = scenes.tiny_scene("conductor")
+    r = setup_renderer(sc, 48, 32, 5, device=0)
+    r.accum_clear()
+    r.render_frames(1, spp)
+    want = r.accum()
+    r.close()
+    np.testing.assert_allclose(got, want, rtol=2e-6, atol=1e-7)
