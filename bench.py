@@ -249,6 +249,14 @@ def main():
                     traffic = tjd.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        valu = None  # the VALU fraction beside the HBM roofline, from PMC passes
+        vj = ROOT / "profiles" / "valu.json"
+        if vj.exists() and dom == "k_extend+k_trace_pair" and args.config == "2":
+            try:
+                vd = json.loads(vj.read_text())
+                valu = {k: vd[k] for k in ("kernel", "valu_busy", "lane_utilisation")}
+            except Exception:
+                valu = None
         out = {
             "metric": "Msamples/sec at 1920x1080, max-depth 8; MSE vs reference",
             "value": round(value, 3),
@@ -298,6 +306,8 @@ def main():
                 "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
                 # SURVEY.md §8(d) whole-path figure: (segments*396 + samples*12) / render time
                 "pipeline_gbps": round(alg_bytes / max(kernel_s, 1e-9) / 1e9, 2),
+                # the bound that actually limits the trace kernel (issue-bound)
+                "valu_pmc": valu,
             },
             "image": {"mean": float(np.nanmean(img) / per_step_spp), "nan_pixels": nan_px},
         }
