@@ -140,9 +140,6 @@ constexpr int kSpillDepth = PT_SPILL_DEPTH;  // spill + LDS hold a BVH4 path of 
 #ifndef PT_TRI_PER_STEP
 #define PT_TRI_PER_STEP 1
 #endif
-#ifndef PT_TRIS_PER_DUAL
-#define PT_TRIS_PER_DUAL 1  // triangles a dual step may test from its leaf
-#endif
 #ifndef PT_SKIP_LAST_SAMPLE
 #define PT_SKIP_LAST_SAMPLE 1  // no BSDF sample on a path's last segment (its ray is never traced)
 #endif
@@ -398,9 +395,6 @@ __device__ __forceinline__ bool trav_step_single(const DevScene& S, TravState& s
 #ifndef PT_NODE_SIGNSEL
 #define PT_NODE_SIGNSEL 1
 #endif
-#ifndef PT_LOAD_FIRST
-#define PT_LOAD_FIRST 0  // 1: a dual step issues its triangle and node loads before either test (slower)
-#endif
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
 // The six sign-selected planes and the child links of one node, as loaded (PT_NODE_SIGNSEL).
@@ -567,35 +561,16 @@ template <int ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                           int* spill, TravStats& ts, bool tri_ok = true) {
 #if PT_DUAL_STEP
-#if PT_LOAD_FIRST && PT_NODE_SIGNSEL
-    // issue the triangle's and the node's loads together (unconditional, clamped to valid
-    // records), so the two L2 round trips of a step overlap instead of following each other
-    const bool do_tri = tri_ok && s.leaf != kEmptyChild;
-    const bool do_node = s.cur >= 0;
-    const int tl = do_tri ? leaf_first(s.leaf) : 0;
-    const float4 TA = S.isect[3 * tl], TE1 = S.isect[3 * tl + 1], TE2 = S.isect[3 * tl + 2];
-    const NodeLoad nl = node_load(S, s, do_node ? s.cur : 0);
-    if (do_tri) {
-        if (leaf_tri_eval<ANY, STATS, TEX>(S, s, ts, TA, TE1, TE2)) return true;
-    }
-    if (do_node) {
-        if (STATS) ts.nodes++;
-        float t0, t1, t2, t3;
-        int c0, c1, c2, c3;
-        node_eval(nl, s, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
-#else
+    // (issuing the triangle and node loads before either test overlaps their round trips but
+    // needs 116 VGPRs, one wave per SIMD fewer: -1.5 % Lambert, -22 % Dielectric)
     if (tri_ok && s.leaf != kEmptyChild) {
         if (leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
-#if PT_TRIS_PER_DUAL > 1
-        if (s.leaf != kEmptyChild && leaf_tri_step<ANY, STATS, TEX>(S, s, ts)) return true;
-#endif
     }
     if (s.cur >= 0) {
         if (STATS) ts.nodes++;
         float t0, t1, t2, t3;
         int c0, c1, c2, c3;
         node_test(S, s, s.cur, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
-#endif
         if ((ANY != kRayAny || !PT_ANY_UNSORTED) && PT_CHILD_SORT > 0) {
             cswap(t0, c0, t1, c1);
             cswap(t2, c2, t3, c3);

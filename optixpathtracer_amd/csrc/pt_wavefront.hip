@@ -52,12 +52,6 @@ constexpr int kMissTri = -1;
 #ifndef PT_HIT_PATH
 #define PT_HIT_PATH 1  // hit records carry the path id instead of t (shading needs no ray_o read)
 #endif
-#ifndef PT_PAIR_BALANCE
-#define PT_PAIR_BALANCE 0  // 1: each k_trace_pair wave takes a share of both ray kinds (slower)
-#endif
-#ifndef PT_PAIR_SPECIALISE
-#define PT_PAIR_SPECIALISE 0  // 1: k_trace_pair runs shadow-only waves in an any-hit loop (slower)
-#endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
@@ -197,16 +191,11 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 #endif
 }
 
-struct IdentityMap {
-    __device__ int operator()(int v) const { return v; }
-};
-
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
-// for ray ri, `finish(ri, state)` consumes a finished ray.  The loop walks positions
-// [next, end); `map` turns a position into the queue index ri.
-template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Map = IdentityMap>
+// for ray ri, `finish(ri, state)` consumes a finished ray.
+template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
 __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TravStats& ts,
-                                            Fetch fetch, Finish finish, Map map = Map()) {
+                                            Fetch fetch, Finish finish) {
     int spill[kSpillDepth];
     TravState st;
     int ri = -1;
@@ -217,7 +206,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         if (__popcll(m) < kRefillMin && m != ~0ull && next < end) m = 0;
         const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         if (need && m && next + pre < end) {
-            ri = map(next + pre);
+            ri = next + pre;
             fetch(ri, st);
             if (STATS) ts.rays++;
             if (S.ntri <= 0) {  // empty scene: no BVH root, every ray misses
@@ -503,37 +492,12 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
                 W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
             }
         };
-#if PT_PAIR_BALANCE
-    // Every wave takes an equal share of BOTH queues (its extension slice, then its shadow
-    // slice): a closest-hit extension ray costs more steps than an any-hit shadow ray, so
-    // contiguous slices of [extension | shadow] would leave the shadow-only waves idle while
-    // the extension waves finish (the grid holds exactly the resident waves).
-    {
-        int e0, e1, s0, s1;
-        wave_slice(n_ext, e0, e1);
-        wave_slice(n_sh, s0, s1);
-        const int ne = e1 - e0;
-        trace_range<kRayMixed, STATS, TEX>(S, 0, ne + (s1 - s0), stk, ts, fetch, finish,
-                                           [=](int v) { return v < ne ? e0 + v : n_ext + s0 + (v - ne); });
-    }
-#else
-    // The queue is [extension rays | shadow rays] and wave slices are contiguous, so all but
-    // one wave trace a single ray kind: those run a loop specialised to it (no child sort and
-    // no closest-hit bookkeeping for shadow rays, no any-hit tests for extension rays).
+    // The queue is [extension rays | shadow rays] in contiguous wave slices, so all but one wave
+    // trace a single ray kind; a mixed-kind loop serves both (per-kind loops in one kernel and
+    // per-wave shares of both kinds were slower).
     int first, end;
     wave_slice(n_ext + n_sh, first, end);
-#if PT_PAIR_SPECIALISE
-    if (first >= n_ext)
-        trace_range<kRayAny, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
-    else
-#endif
-#if PT_PAIR_SPECIALISE > 1
-    if (end <= n_ext)
-        trace_range<kRayClosest, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
-    else
-#endif
-        trace_range<kRayMixed, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
-#endif
+    trace_range<kRayMixed, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
