@@ -458,3 +458,18 @@ def test_launch_params_matches_render():
     r.launch(0, (0, 0), 1, p, iv, ip, 0, 0, depth)  # empty grid: no-op
     r.close()
     hb.free()
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_fullhd_largest_batch_bit_identical(diffuse_scene, mode):
+    """Maximum queue size at the headline resolution: 1920x1080 with frames_per_launch far
+    above the renderer's cap of 2^28 paths per batch (129 frames, 45 GB of queues: one batch of
+    129 frames and a ragged one of 1) gives the accumulator of 64-frame batches (64 + 64 + 2)
+    bit for bit, with the same segment count."""
+    n = 130
+    ref, sr = gpu_render(diffuse_scene, 1920, 1080, 8, 1, n, mode=mode, kernel=1, frames_per_launch=64)
+    big, sb = gpu_render(diffuse_scene, 1920, 1080, 8, 1, n, mode=mode, kernel=1, frames_per_launch=4096)
+    np.testing.assert_array_equal(big, ref)
+    assert sb["segments"] == sr["segments"]
+    assert np.isfinite(ref).all()
+    assert sr["samples"] == 1920 * 1080 * n
