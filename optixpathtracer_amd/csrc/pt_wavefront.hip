@@ -199,11 +199,16 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
     int spill[kSpillDepth];
     TravState st;
     int ri = -1;
+    // the slice bounds are wave-uniform: keeping them (and the refill bookkeeping) in SGPRs
+    // makes the per-step refill test scalar work (it was VALU, with an f64 min from the
+    // unsigned popcount; ±0.3 %)
+    next = __builtin_amdgcn_readfirstlane(next);
+    end = __builtin_amdgcn_readfirstlane(end);
     while (true) {
         const bool need = ri < 0;
         unsigned long long m = __ballot(need ? 1 : 0);
         // refill once enough lanes idle (the refill block costs the wave as much as a step)
-        if (__popcll(m) < kRefillMin && m != ~0ull && next < end) m = 0;
+        if ((int)__popcll(m) < kRefillMin && next < end) m = 0;  // (< kRefillMin lanes: m != ~0)
         const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         if (need && m && next + pre < end) {
             ri = next + pre;
@@ -214,7 +219,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
                 ri = -1;
             }
         }
-        next = min(next + __popcll(m), end);
+        next = min(next + (int)__popcll(m), end);
         const unsigned long long act = __ballot(ri >= 0 ? 1 : 0);
         if (!act) break;
 #if PT_DUAL_STEP && PT_TRI_BATCH > 0
