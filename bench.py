@@ -257,6 +257,14 @@ def main():
                 valu = {k: vd[k] for k in ("kernel", "valu_busy", "lane_utilisation")}
             except Exception:
                 valu = None
+        shade = None  # the memory-bound kernel of a Lambert frame, PMC HBM GB/s (tools/shade_pmc.py)
+        sj = ROOT / "profiles" / "shade_pmc.json"
+        if sj.exists() and dom == "k_extend+k_trace_pair" and args.config == "2":
+            try:
+                sk = json.loads(sj.read_text())["kernels"]["k_shade_fused<1, false>"]
+                shade = {"kernel": "k_shade_fused<Lambert>", **{k: sk[k] for k in ("hbm_gbps", "frac", "avg_launch_ms")}}
+            except Exception:
+                shade = None
         out = {
             "metric": "Msamples/sec at 1920x1080, max-depth 8; MSE vs reference",
             "value": round(value, 3),
@@ -308,6 +316,8 @@ def main():
                 "pipeline_gbps": round(alg_bytes / max(kernel_s, 1e-9) / 1e9, 2),
                 # the bound that actually limits the trace kernel (issue-bound)
                 "valu_pmc": valu,
+                # PMC HBM bandwidth of the shading kernel (2 x FETCH_SIZE + WRITE_SIZE per launch)
+                "shade_pmc": shade,
             },
             "image": {"mean": float(np.nanmean(img) / per_step_spp), "nan_pixels": nan_px},
         }
