@@ -191,6 +191,29 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 #endif
 }
 
+// k_shade_fused (the memory-bound kernel of a fused-mode frame, ≈ 66 % of HBM peak) streams
+// its queue records once: non-temporal loads (1) and stores (1, 2) keep them from evicting the
+// triangle and material lines its gathers reuse.  Lambert +1.7 %, Dielectric and Conductor
+// +0.4 %.
+#ifndef PT_NT_SHADE
+#define PT_NT_SHADE 1
+#endif
+__device__ __forceinline__ float4 ldqs(const float4* p) {
+#if PT_NT_SHADE == 1
+    const pt_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pt_v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stqs(float4* p, float4 v) {
+#if PT_NT_SHADE
+    __builtin_nontemporal_store(pt_v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<pt_v4f*>(p));
+#else
+    *p = v;
+#endif
+}
+
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
@@ -378,11 +401,11 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
         float stmax = 0.0f;
         int path = 0;
         if (valid) {
-            const float4 hv = W.hit[i];
+            const float4 hv = ldqs(W.hit + i);
             path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
             const Hit h = decode_hit(hv);
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
-                const float4 c = rd[i];
+                const float4 c = ldqs(rd + i);
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
@@ -430,14 +453,14 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
         }
         const int si = block_append(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
         if (emit_shadow) {
-            W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(path));
-            W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
-            W.sh_c[si] = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+            stqs(W.sh_o + si, make_float4(so.x, so.y, so.z, __int_as_float(path)));
+            stqs(W.sh_d + si, make_float4(sdir.x, sdir.y, sdir.z, stmax));
+            stqs(W.sh_c + si, make_float4(contrib.x, contrib.y, contrib.z, 0.0f));
         }
         const int qi = block_append(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
-            no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
-            nd[qi] = make_float4(d.x, d.y, d.z, 0.0f);
+            stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
+            stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
         }
     }
 }
