@@ -198,6 +198,9 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 #ifndef PT_NT_SHADE
 #define PT_NT_SHADE 1
 #endif
+#ifndef PT_NT_BETA
+#define PT_NT_BETA 1  // also the path state read-modify-write (+0.3 % Lambert and Conductor, 4 rounds)
+#endif
 __device__ __forceinline__ float4 ldqs(const float4* p) {
 #if PT_NT_SHADE == 1
     const pt_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pt_v4f*>(p));
@@ -409,7 +412,11 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
+                #if PT_NT_BETA
+                float4 bv = ldqs(W.beta + path);
+#else
                 float4 bv = W.beta[path];
+#endif
                 uint32_t seed = __float_as_uint(bv.w);
                 f3 beta = mk(bv.x, bv.y, bv.z);
                 const bool conductor = rnd(seed) < sf.metallic;  // :400
@@ -447,7 +454,11 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 if ((!PT_SKIP_LAST_SAMPLE || b + 1 < L.max_bounces) &&
                     bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
                     emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
+                    #if PT_NT_BETA
+                    stqs(W.beta + path, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
+#else
                     W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
+#endif
                 }
             }
         }
