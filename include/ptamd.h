@@ -114,6 +114,9 @@ typedef struct pt_stats {
     uint64_t trace_kernel_bytes; /* their algorithmic queue bytes: 32 B per ray read + 16 B per
                                     hit / shadow record written (k_extend with primary dedup
                                     writes one record per frame of the batch) */
+    uint64_t strict_retraces;    /* rays traced a second time because their first answer was a hit
+                                    outside the triangle's own box (pt_device.h tri_accept; counted
+                                    while pt_set_traversal_stats(r, 1)) */
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -219,6 +222,10 @@ int pt_camera_from_blender(const float blender_position[3], const float blender_
  * the LBVH.  prim = global triangle index (meshes concatenated) or -1. */
 int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* prim, float* t,
                   float* u, float* v, int32_t* backface, int32_t any_hit);
+
+/* Debug / determinism: copy the BVH4 node array (128 B per node, pt_stats.bvh_nodes nodes) and
+ * the leaf-ordered triangle records (48 B per triangle) to host; at most the given byte counts. */
+int pt_bvh_download(pt_renderer* r, void* nodes, int64_t node_bytes, void* triangles, int64_t triangle_bytes);
 
 const char* pt_last_error(void);
 const char* pt_version(void);

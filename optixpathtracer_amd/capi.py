@@ -97,6 +97,7 @@ class pt_stats(C.Structure):
         ("shadow_rays", C.c_uint64),
         ("trace_kernel_rays", C.c_uint64),
         ("trace_kernel_bytes", C.c_uint64),
+        ("strict_retraces", C.c_uint64),
     ]
 
 
@@ -153,6 +154,7 @@ SIGNATURES = {
     "pt_stats_reset": (C.c_int, [_R]),
     "pt_camera_from_blender": (C.c_int, [_FP, _FP, C.c_float, C.c_int32, C.c_int32, _FP, _FP, _FP]),
     "pt_trace_rays": (C.c_int, [_R, _FP, C.c_int32, _IP, _FP, _FP, _FP, _IP, C.c_int32]),
+    "pt_bvh_download": (C.c_int, [_R, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]),
     "pt_last_error": (C.c_char_p, []),
     "pt_version": (C.c_char_p, []),
     "pt_display_reset": (C.c_int, [_R, C.c_int32]),

@@ -8,19 +8,21 @@
 //   4. k_sparse   : sparse-table level l = union of two level l-1 boxes (log2 N launches)
 //   5. k_karras   : binary LBVH, one thread per internal node (Karras 2012 split search);
 //                   each node's AABB = O(1) sparse-table range query over its leaf range
-//   6. k_collapse : top-down, one launch per BVH4 level: each BVH4 node greedily opens its
-//                   largest-area binary child until it has 4 children; a binary subtree of
-//                   <= kLeafMax triangles (a contiguous leaf range) becomes a BVH4 leaf.
+//   6. SAH-optimal BVH4 collapse: a bottom-up dynamic programme (k_sah_dp) picks every binary
+//                   node's cheapest cover by 1-4 BVH4 children, a top-down pass replays it one
+//                   BVH4 level at a time (k_collapse_count -> scan -> k_collapse_emit), numbering
+//                   the nodes breadth-first by a prefix sum: the node array is the same on every
+//                   build (no atomic slot order), and the top levels are a contiguous prefix.
 // PLOC builder (Meister & Bittner 2018, "Parallel Locally-Ordered Clustering for Bounding
 // Volume Hierarchy Construction"), the default: starting from the Morton-sorted leaves, each
 // iteration finds every cluster's nearest neighbour (smallest merged surface area) within
 // +-kPlocRadius positions, merges mutual pairs and compacts (hipCUB scan).  A top-down pass
 // then numbers the leaves in depth-first order, so every subtree is again a contiguous
-// leaf range, and the same k_collapse turns it into BVH4.  Its SAH quality is close to a
+// leaf range, and the same collapse turns it into BVH4.  Its SAH quality is close to a
 // full sweep build, which cuts traversal steps against the Karras tree.
-// Every kernel reads only what earlier launches wrote (no intra-launch hand-offs), so the
-// build needs no agent-scope fences; node numbering depends on atomic order but the
-// traversal result does not (closest hit is ordered by (t, triangle index)).  The sparse
+// Apart from the DP's bottom-up hand-off, every kernel reads only what earlier launches wrote.
+// The build is deterministic: the same scene gives the same node and triangle arrays bit for
+// bit (tests/test_gpu_parity.py::test_bvh_build_deterministic).  The sparse
 // table costs N*log2(N)*32 B (~150 MB at 250k triangles) — trivial against 288 GB HBM.
 #include <hipcub/hipcub.hpp>
 
@@ -48,6 +50,15 @@ __device__ __forceinline__ void tri_box(const float4* tri, int i, float lo[3], f
     hi[0] = fmaxf(fmaxf(a.x, b.x), c.x);
     hi[1] = fmaxf(fmaxf(a.y, b.y), c.y);
     hi[2] = fmaxf(fmaxf(a.z, b.z), c.z);
+}
+
+// The box the traversal's hit-acceptance rule uses for triangle i (pt_device.h tri_accept): the
+// vertices as the hit test sees them (v0, v0 + (v1 - v0), v0 + (v2 - v0)), padded.  All BVH
+// boxes are unions of these, so they contain every acceptance box bit for bit.
+__device__ __forceinline__ void tri_box_accept(const float4* tri, int i, float lo[3], float hi[3]) {
+    const float4 a = tri[3 * i], b = tri[3 * i + 1], c = tri[3 * i + 2];
+    const f3 v0 = mk(a.x, a.y, a.z);
+    tri_box_padded(v0, mk(b.x - a.x, b.y - a.y, b.z - a.z), mk(c.x - a.x, c.y - a.y, c.z - a.z), lo, hi);
 }
 
 __global__ void k_morton(const float4* tri, int n, float3 cmin, float3 cinv, uint32_t* keys, uint32_t* vals) {
@@ -86,7 +97,7 @@ __global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const f
     shade[4 * k + 2] = make_float4(na.z, nb.x, nb.y, nb.z);
     shade[4 * k + 3] = make_float4(nc.x, nc.y, nc.z, 0.0f);
     float lo[3], hi[3];
-    tri_box(tri_orig, i, lo, hi);
+    tri_box_accept(tri_orig, i, lo, hi);
     st0[2 * k] = make_float4(lo[0], lo[1], lo[2], 0.0f);
     st0[2 * k + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
 }
@@ -178,88 +189,7 @@ __device__ __forceinline__ float half_area(float4 lo, float4 hi) {
     float x = hi.x - lo.x, y = hi.y - lo.y, z = hi.z - lo.z;
     return x * y + y * z + z * x;
 }
-// Conservative padding so the traversal's fma slab test never culls a true hit.
-__device__ __forceinline__ float pad_amount(float x) { return fabsf(x) * 9.5367431640625e-7f + 1e-6f; }
-
-// One BVH4 node per work item: (binary code, BVH4 slot).
-__global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, int* counter, int2* next,
-                           int* nnext) {
-    int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nwork) return;
-    const int2 item = work[w];
-    int c[4];
-    int n;
-    if (item.x >= 0) {
-        int2 ch = B.child[item.x];
-        c[0] = ch.x;
-        c[1] = ch.y;
-        n = 2;
-    } else {  // degenerate scene: the root is a single leaf
-        c[0] = item.x;
-        n = 1;
-    }
-    while (n < 4) {  // open the largest-area child that cannot be a leaf
-        int best = -1;
-        float ba = -1.0f;
-        for (int k = 0; k < n; ++k) {
-            if (c[k] < 0 || code_count(B, c[k]) <= kLeafMax) continue;
-            float4 lo, hi;
-            code_box(B, c[k], lo, hi);
-            float a = half_area(lo, hi);
-            if (a > ba) {
-                ba = a;
-                best = k;
-            }
-        }
-        if (best < 0) break;
-        int2 ch = B.child[c[best]];
-        c[best] = ch.x;
-        c[n++] = ch.y;
-    }
-    float lo[3][4], hi[3][4];
-    int cc[4];
-    for (int k = 0; k < 4; ++k) {
-        if (k >= n) {
-            cc[k] = kEmptyChild;
-            // inverted box: misses for every ray direction (the sign-selected slab test of
-            // pt_device.h node_test relies on it instead of testing the child id)
-            for (int a = 0; a < 3; ++a) {
-                lo[a][k] = __int_as_float(0x7f800000);
-                hi[a][k] = -__int_as_float(0x7f800000);
-            }
-            continue;
-        }
-        float4 l4, h4;
-        code_box(B, c[k], l4, h4);
-        float l[3] = {l4.x, l4.y, l4.z}, h[3] = {h4.x, h4.y, h4.z};
-        for (int a = 0; a < 3; ++a) {
-            lo[a][k] = l[a] - pad_amount(l[a]);
-            hi[a][k] = h[a] + pad_amount(h[a]);
-        }
-        int cnt = code_count(B, c[k]);
-        if (cnt <= kLeafMax) {
-            cc[k] = ~((code_first(B, c[k]) << 3) | (cnt - 1));
-        } else {
-            int slot = atomicAdd(counter, 1);
-            cc[k] = slot;
-            int q = atomicAdd(nnext, 1);
-            next[q] = make_int2(c[k], slot);
-        }
-    }
-    BNode4 nd;
-    nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
-    nd.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
-    nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
-    nd.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
-    nd.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
-    nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
-    nd.child = make_int4(cc[0], cc[1], cc[2], cc[3]);
-    nd.pad = make_int4(0, 0, 0, 0);
-    out[item.y] = nd;
-}
-
-
-// ---- SAH-optimal BVH4 collapse (default; PT_SAH_COLLAPSE=0 restores the greedy one) --------
+// ---- SAH-optimal BVH4 collapse -------------------------------------------------------------
 // Bottom-up dynamic programme over the binary tree (the wide-BVH collapse of Ylitie, Karras &
 // Laine 2017, "Efficient Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs",
 // for 4-wide nodes): cost[n][j] = cheapest SAH cost of covering subtree n with at most j
@@ -269,9 +199,6 @@ __global__ void k_collapse(BinTree B, const int2* work, int nwork, BNode4* out, 
 //   cost[n][1] = single(n);  cost[n][j] = min(single(n), min_a cost[L][a] + cost[R][j - a])
 // The top-down k_collapse_sah then replays the recorded choices.  With the dual traversal
 // step (pt_device.h) a triangle test overlaps a node visit, hence cTri < cNode.
-#ifndef PT_SAH_COLLAPSE
-#define PT_SAH_COLLAPSE 1
-#endif
 #ifndef PT_SAH_LEAF_MAX
 #define PT_SAH_LEAF_MAX 4
 #endif
@@ -365,61 +292,83 @@ __global__ void k_sah_dp(BinTree B, int n, const int* parent, const int* leafpar
     }
 }
 
-// One BVH4 node per work item (binary code, BVH4 slot): children from the DP choices.
-__global__ void k_collapse_sah(BinTree B, const int* dpd, const int2* work, int nwork, BNode4* out, int* counter,
-                               int2* next, int* nnext) {
+// Children of one BVH4 node (work item: binary code) from the DP choices, in DFS order of the
+// binary tree; returns the count (1..4).
+__device__ __forceinline__ int collapse_children(const BinTree& B, const int* dpd, int code, int c[4]) {
+    int n = 0;
+    if (code < 0) {  // degenerate scene: the root is a single leaf
+        c[n++] = code;
+        return n;
+    }
+    int st_code[8], st_j[8], sp = 0;
+    const int2 ch = B.child[code];
+    const int a = dp_node_split(dpd[code]);
+    st_code[sp] = ch.y; st_j[sp++] = 4 - a;
+    st_code[sp] = ch.x; st_j[sp++] = a;
+    while (sp > 0) {
+        --sp;
+        const int x = st_code[sp], j = st_j[sp];
+        const int s = (x < 0 || j < 2) ? 0 : dp_split(dpd[x], j);
+        if (s == 0) {
+            c[n++] = x;
+        } else {
+            const int2 xc = B.child[x];
+            st_code[sp] = xc.y; st_j[sp++] = j - s;
+            st_code[sp] = xc.x; st_j[sp++] = s;
+        }
+    }
+    return n;
+}
+__device__ __forceinline__ bool child_is_leaf(const BinTree& B, const int* dpd, int code) {
+    return code < 0 || dp_is_leaf(dpd[code]);
+}
+
+// Top-down collapse, one BVH4 level per launch pair.  k_collapse_count: inner (non-leaf)
+// children per work item; an exclusive scan of the counts gives every inner child its slot
+// (level base + offset) and its position in the next level's work list, so the numbering is
+// breadth-first and the same on every build.
+__global__ void k_collapse_count(BinTree B, const int* dpd, const int* work, int nwork, int* cnt) {
     int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nwork) return;
-    const int2 item = work[w];
     int c[4];
-    int n = 0;
-    if (item.x >= 0) {
-        int st_code[8], st_j[8], sp = 0;
-        const int2 ch = B.child[item.x];
-        const int a = dp_node_split(dpd[item.x]);
-        st_code[sp] = ch.y; st_j[sp++] = 4 - a;
-        st_code[sp] = ch.x; st_j[sp++] = a;
-        while (sp > 0) {
-            --sp;
-            const int x = st_code[sp], j = st_j[sp];
-            const int s = (x < 0 || j < 2) ? 0 : dp_split(dpd[x], j);
-            if (s == 0) {
-                c[n++] = x;
-            } else {
-                const int2 xc = B.child[x];
-                st_code[sp] = xc.y; st_j[sp++] = j - s;
-                st_code[sp] = xc.x; st_j[sp++] = s;
-            }
-        }
-    } else {  // degenerate scene: the root is a single leaf
-        c[n++] = item.x;
-    }
+    const int n = collapse_children(B, dpd, work[w], c);
+    int inner = 0;
+    for (int k = 0; k < n; ++k) inner += child_is_leaf(B, dpd, c[k]) ? 0 : 1;
+    cnt[w] = inner;
+}
+
+// k_collapse_emit: node of work item w goes to slot level_base + w (the parent assigned it
+// in this order), its inner children to next_base + off[w] + j.
+__global__ void k_collapse_emit(BinTree B, const int* dpd, const int* work, int nwork, const int* off,
+                                int level_base, int next_base, BNode4* out, int* next) {
+    int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwork) return;
+    int c[4];
+    const int n = collapse_children(B, dpd, work[w], c);
     float lo[3][4], hi[3][4];
     int cc[4];
+    int j = off[w];
     for (int k = 0; k < 4; ++k) {
         if (k >= n) {
             cc[k] = kEmptyChild;
-            for (int a = 0; a < 3; ++a) {  // inverted box: never hit (see k_collapse)
+            // inverted box: misses for every ray direction (the sign-selected slab test of
+            // pt_device.h node_eval relies on it instead of testing the child id)
+            for (int a = 0; a < 3; ++a) {
                 lo[a][k] = __int_as_float(0x7f800000);
                 hi[a][k] = -__int_as_float(0x7f800000);
             }
             continue;
         }
-        float4 l4, h4;
+        float4 l4, h4;  // already the union of padded acceptance boxes (tri_box_accept)
         code_box(B, c[k], l4, h4);
-        float l[3] = {l4.x, l4.y, l4.z}, h[3] = {h4.x, h4.y, h4.z};
-        for (int a = 0; a < 3; ++a) {
-            lo[a][k] = l[a] - pad_amount(l[a]);
-            hi[a][k] = h[a] + pad_amount(h[a]);
-        }
-        const bool leaf = c[k] < 0 || dp_is_leaf(dpd[c[k]]);
-        if (leaf) {
+        lo[0][k] = l4.x; lo[1][k] = l4.y; lo[2][k] = l4.z;
+        hi[0][k] = h4.x; hi[1][k] = h4.y; hi[2][k] = h4.z;
+        if (child_is_leaf(B, dpd, c[k])) {
             cc[k] = ~((code_first(B, c[k]) << 3) | (code_count(B, c[k]) - 1));
         } else {
-            int slot = atomicAdd(counter, 1);
-            cc[k] = slot;
-            int q = atomicAdd(nnext, 1);
-            next[q] = make_int2(c[k], slot);
+            cc[k] = next_base + j;
+            next[j] = c[k];
+            ++j;
         }
     }
     BNode4 nd;
@@ -431,7 +380,7 @@ __global__ void k_collapse_sah(BinTree B, const int* dpd, const int2* work, int 
     nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
     nd.child = make_int4(cc[0], cc[1], cc[2], cc[3]);
     nd.pad = make_int4(0, 0, 0, 0);
-    out[item.y] = nd;
+    out[level_base + w] = nd;
 }
 
 // ---- PLOC ---------------------------------------------------------------------------------
@@ -452,7 +401,7 @@ __global__ void k_leafbox(const float4* tri_orig, const uint32_t* order, int n, 
     int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n) return;
     float lo[3], hi[3];
-    tri_box(tri_orig, (int)order[m], lo, hi);
+    tri_box_accept(tri_orig, (int)order[m], lo, hi);
     box[2 * m] = make_float4(lo[0], lo[1], lo[2], 0.0f);
     box[2 * m + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
     code[m] = ~m;
@@ -669,18 +618,17 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     hipError_t err = hipSuccess;
     uint32_t *keys = nullptr, *vals = nullptr, *keys2 = nullptr, *vals2 = nullptr;
     float4 *st = nullptr, *bbox = nullptr;
-    int2 *bchild = nullptr, *brange = nullptr, *work = nullptr, *work2 = nullptr;
-    int* cnt = nullptr;  // [0] node counter, [1] next-level work count
+    int2 *bchild = nullptr, *brange = nullptr;
+    int *work = nullptr, *work2 = nullptr, *wcnt = nullptr, *woff = nullptr;
     int *dp_parent = nullptr, *dp_leafparent = nullptr, *dp_visits = nullptr, *dp_dec = nullptr;
     float4* dp_cost = nullptr;
     void* temp = nullptr;
-    size_t temp_bytes = 0;
+    size_t temp_bytes = 0, scan_bytes = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int levels = 1;
     SparseTable table{};
     BinTree B{};
-    int h_cnt[2] = {1, 0};
-    int nwork = 1, depth = 0, root = 0;
+    int nwork = 1, depth = 0, root = 0, node_count = 1, level_base = 0;
     const int nbin = n > 1 ? n - 1 : 1;
     const bool ploc = in.builder != kBuilderLBVH;
     std::vector<void*> owned;
@@ -701,10 +649,13 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
         PT_TRY(hipMalloc(&brange, sizeof(int2) * nbin));
         PT_TRY(hipMalloc(&bbox, sizeof(float4) * 2 * nbin));
     }
-    PT_TRY(hipMalloc(&work, sizeof(int2) * n));
-    PT_TRY(hipMalloc(&work2, sizeof(int2) * n));
-    PT_TRY(hipMalloc(&cnt, sizeof(int) * 2));
+    PT_TRY(hipMalloc(&work, sizeof(int) * n));
+    PT_TRY(hipMalloc(&work2, sizeof(int) * n));
+    PT_TRY(hipMalloc(&wcnt, sizeof(int) * n));
+    PT_TRY(hipMalloc(&woff, sizeof(int) * n));
     PT_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, n, 0, 30, stream));
+    PT_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, wcnt, woff, n, stream));
+    temp_bytes = std::max(temp_bytes, scan_bytes);
     PT_TRY(hipMalloc(&temp, temp_bytes > 0 ? temp_bytes : 16));
     PT_TRY(hipEventRecord(e0, stream));
     {
@@ -744,7 +695,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             B.leafbox = st;
             root = n > 1 ? 0 : ~0;
         }
-        if (PT_SAH_COLLAPSE && root >= 0) {  // SAH DP over the binary tree (n >= 2)
+        if (root >= 0) {  // SAH DP over the binary tree (n >= 2)
             PT_TRY(hipMalloc(&dp_parent, sizeof(int) * nbin));
             PT_TRY(hipMalloc(&dp_leafparent, sizeof(int) * n));
             PT_TRY(hipMalloc(&dp_visits, sizeof(int) * nbin));
@@ -759,37 +710,36 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
                                dp_visits, dp_cost, dp_dec);
             PT_TRY(hipGetLastError());
         }
-        // root work item: binary root (or the single leaf ~0) -> BVH4 slot 0
-        int2 rw = make_int2(root, 0);
-        PT_TRY(hipMemcpyAsync(work, &rw, sizeof(int2), hipMemcpyHostToDevice, stream));
-        PT_TRY(hipMemcpyAsync(cnt, h_cnt, sizeof(int) * 2, hipMemcpyHostToDevice, stream));
+        // level 0: the binary root (or the single leaf ~0) -> BVH4 slot 0
+        PT_TRY(hipMemcpyAsync(work, &root, sizeof(int), hipMemcpyHostToDevice, stream));
         while (nwork > 0) {
-            PT_TRY(hipMemsetAsync(cnt + 1, 0, sizeof(int), stream));
-            if (dp_dec)
-                hipLaunchKernelGGL(k_collapse_sah, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, dp_dec, work,
-                                   nwork, out.nodes, cnt, work2, cnt + 1);
-            else
-                hipLaunchKernelGGL(k_collapse, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, work, nwork,
-                                   out.nodes, cnt, work2, cnt + 1);
+            hipLaunchKernelGGL(k_collapse_count, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, dp_dec, work,
+                               nwork, wcnt);
             PT_TRY(hipGetLastError());
-            PT_TRY(hipMemcpyAsync(h_cnt, cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
+            PT_TRY(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, wcnt, woff, nwork, stream));
+            hipLaunchKernelGGL(k_collapse_emit, dim3(grid_for(nwork, 128)), dim3(128), 0, stream, B, dp_dec, work,
+                               nwork, woff, level_base, node_count, out.nodes, work2);
+            PT_TRY(hipGetLastError());
+            int tail[2] = {0, 0};  // offset and count of the level's last item: the next level's size
+            PT_TRY(hipMemcpyAsync(&tail[0], woff + nwork - 1, sizeof(int), hipMemcpyDeviceToHost, stream));
+            PT_TRY(hipMemcpyAsync(&tail[1], wcnt + nwork - 1, sizeof(int), hipMemcpyDeviceToHost, stream));
             PT_TRY(hipStreamSynchronize(stream));
-            nwork = h_cnt[1];
+            nwork = tail[0] + tail[1];
+            level_base = node_count;
+            node_count += nwork;
             ++depth;
-            int2* t = work;
-            work = work2;
-            work2 = t;
+            std::swap(work, work2);
         }
     }
     PT_TRY(hipEventRecord(e1, stream));
     PT_TRY(hipEventSynchronize(e1));
     if (ms) PT_TRY(hipEventElapsedTime(ms, e0, e1));
-    out.n_nodes = h_cnt[0];
+    out.n_nodes = node_count;
     out.depth = depth;
 done:
     (void)hipStreamSynchronize(stream);
     for (void* p : {(void*)keys, (void*)vals, (void*)keys2, (void*)vals2, (void*)st, (void*)bchild, (void*)brange,
-                    (void*)bbox, (void*)work, (void*)work2, (void*)cnt, temp, (void*)dp_parent,
+                    (void*)bbox, (void*)work, (void*)work2, (void*)wcnt, (void*)woff, temp, (void*)dp_parent,
                     (void*)dp_leafparent, (void*)dp_visits, (void*)dp_cost, (void*)dp_dec})
         if (p) (void)hipFree(p);
     for (void* p : owned) (void)hipFree(p);

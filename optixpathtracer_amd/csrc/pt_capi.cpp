@@ -82,6 +82,11 @@ struct EventPool {
     }
 };
 
+// Device counters: [0] segments [1] nodes visited [2] triangle tests [3] rays [4] stack
+// overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces.
+constexpr int kCounters = 16;
+constexpr int kMinTraversalStack = 16 + kSpillDepth;  // pt_wavefront.hip kStack + pt_device.h kSpillDepth
+
 }  // namespace
 
 struct pt_renderer {
@@ -399,8 +404,8 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         if (e__ != hipSuccess) return cleanup_fail(hip_fail(e__, where)); \
     } while (0)
     PT_HIPC(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking), "hipStreamCreate");
-    PT_HIPC(hipMalloc(&r->d_counters, 8 * sizeof(unsigned long long)), "hipMalloc counters");
-    PT_HIPC(hipMemsetAsync(r->d_counters, 0, 8 * sizeof(unsigned long long), r->stream), "hipMemset");
+    PT_HIPC(hipMalloc(&r->d_counters, kCounters * sizeof(unsigned long long)), "hipMalloc counters");
+    PT_HIPC(hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream), "hipMemset");
     PT_HIPC(hipMalloc(&r->d_mats, sizeof(float4) * mats.size()), "hipMalloc mats");
     PT_HIPC(hipMemcpyAsync(r->d_mats, mats.data(), sizeof(float4) * mats.size(), hipMemcpyHostToDevice, r->stream),
             "upload mats");
@@ -460,6 +465,11 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         r->bvh_ms = ms;
         r->bvh_nodes = bo.n_nodes;
         r->bvh_depth = bo.depth;
+        // a traversal holds at most 3 stack entries per BVH4 level; the smallest traversal stack
+        // (wavefront: 16 LDS + 64 spill entries) must hold them, or rays could lose subtrees
+        if (3 * bo.depth > kMinTraversalStack)
+            return cleanup_fail(fail(PT_ERR_INVALID, "pt_create: BVH too deep for the traversal stack (depth " +
+                                                         std::to_string(bo.depth) + ")"));
     }
     PT_HIPC(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
 #undef PT_HIPC
@@ -731,7 +741,7 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     if (!r || !out) return fail(PT_ERR_INVALID, "pt_get_stats: NULL");
     int rc = pt_synchronize(r);
     if (rc) return rc;
-    unsigned long long c[8];
+    unsigned long long c[kCounters];
     PT_HIP(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost), "download counters");
     std::memset(out, 0, sizeof *out);
     out->segments = c[0];
@@ -754,6 +764,7 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->shadow_rays = c[5];
     out->trace_kernel_rays = c[6];
     out->trace_kernel_bytes = c[7];
+    out->strict_retraces = c[8];
     return PT_OK;
 }
 
@@ -761,7 +772,7 @@ int pt_stats_reset(pt_renderer* r) {
     if (!r) return fail(PT_ERR_INVALID, "pt_stats_reset: NULL");
     int rc = pt_synchronize(r);
     if (rc) return rc;
-    PT_HIP(hipMemset(r->d_counters, 0, 8 * sizeof(unsigned long long)), "hipMemset counters");
+    PT_HIP(hipMemset(r->d_counters, 0, kCounters * sizeof(unsigned long long)), "hipMemset counters");
     r->samples = 0;
     r->last_ms = r->total_ms = 0.0;
     r->calls = 0;
@@ -887,6 +898,20 @@ int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* pr
 }
 
 }  // extern "C"
+
+extern "C" int pt_bvh_download(pt_renderer* r, void* nodes, int64_t node_bytes, void* triangles,
+                               int64_t triangle_bytes) {
+    if (!r || node_bytes < 0 || triangle_bytes < 0 || (node_bytes > 0 && !nodes) ||
+        (triangle_bytes > 0 && !triangles))
+        return fail(PT_ERR_INVALID, "pt_bvh_download: invalid");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    const int64_t nb = std::min<int64_t>(node_bytes, (int64_t)sizeof(BNode4) * r->bvh_nodes);
+    const int64_t tb = std::min<int64_t>(triangle_bytes, (int64_t)sizeof(float4) * 3 * r->ntri);
+    if (nb > 0) PT_HIP(hipMemcpy(nodes, r->d_nodes, (size_t)nb, hipMemcpyDeviceToHost), "download nodes");
+    if (tb > 0) PT_HIP(hipMemcpy(triangles, r->d_isect, (size_t)tb, hipMemcpyDeviceToHost), "download triangles");
+    return PT_OK;
+}
 
 extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_traversal_stats: NULL");

@@ -11,17 +11,13 @@
 //                                  the same fp32 subtraction the oracle performs)
 //   shade  : float4[4N]         — v1.xyz|n0.x, v2.xyz|n0.y, n0.z n1.xyz, n2.xyz|0
 //   mats   : float4[2M]         — albedo.xyz|metallic, roughness|has_normals|0|0
-// Leaves reference up to kLeafMax consecutive triangles (an LBVH subtree is a contiguous
-// range of the Morton-sorted triangles, so no index indirection is needed).
+// Leaves reference up to 4 consecutive triangles (a BVH subtree is a contiguous range of the
+// leaf-ordered triangles, so no index indirection is needed).
 #pragma once
 #include "pt_bsdf.h"
 
 namespace pt {
 
-#ifndef PT_LEAF_MAX
-#define PT_LEAF_MAX 2
-#endif
-constexpr int kLeafMax = PT_LEAF_MAX;
 constexpr int kEmptyChild = (int)0x80000000;
 
 struct __align__(16) BNode4 {
@@ -75,44 +71,53 @@ struct Hit {
 };
 
 struct TravStats {
-    uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0;
+    uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0, retrace = 0;
 };
 
-// Reciprocal direction; zero components map to a huge finite value so the fma slab form
-// never produces 0*inf.
-#ifndef PT_CHILD_SORT
-#define PT_CHILD_SORT 2  // 2: full 4-sort of the hit children; 1: nearest first only; 0: none
-#endif
-#ifndef PT_ANY_UNSORTED
-#define PT_ANY_UNSORTED 1
-#endif
-#ifndef PT_FAST_RCP
-#define PT_FAST_RCP 1
-#endif
-__device__ __forceinline__ float slab_rcp(float x) {
-#if PT_FAST_RCP
-    return __builtin_amdgcn_rcpf(x);  // 1 ulp; covered by the box padding and tfar widening
-#else
-    return 1.0f / x;
-#endif
-}
-__device__ __forceinline__ f3 safe_inv(f3 d) {
-    const float big = 1e30f;
-    return mk(d.x != 0.0f ? slab_rcp(d.x) : copysignf(big, d.x), d.y != 0.0f ? slab_rcp(d.y) : copysignf(big, d.y),
-              d.z != 0.0f ? slab_rcp(d.z) : copysignf(big, d.z));
+// ---- ray / box arithmetic shared bit for bit with the oracle ---------------------------------
+// The slab distance of a plane p on axis a is fma(p, inv_a, -io_a) with inv = 1/d (IEEE
+// division; a zero component maps to +-1e30) and io = o * inv.  oracle/pt_oracle.c evaluates
+// the same expressions, so both sides agree bit for bit on every slab distance, and with it on
+// the hit-acceptance rule below.
+constexpr float kSlabWiden = 1.000244140625f;  // 1 + 2^-12, see tri_accept
+__device__ __forceinline__ float ray_inv(float d) { return d != 0.0f ? 1.0f / d : copysignf(1e30f, d); }
+__device__ __forceinline__ f3 safe_inv(f3 d) { return mk(ray_inv(d.x), ray_inv(d.y), ray_inv(d.z)); }
+
+// Padded box of one triangle, from the vertices exactly as the hit test sees them (v0, v0 + e1,
+// v0 + e2, with e = v - v0 rounded once).  The BVH builder (pt_build.hip) unions these boxes,
+// so every BVH box holding a triangle contains this box bit for bit.
+PT_HD float box_pad(float x) { return fabsf(x) * 9.5367431640625e-7f + 1e-6f; }
+PT_HD void tri_box_padded(f3 v0, f3 e1, f3 e2, float lo[3], float hi[3]) {
+    const float a[3] = {v0.x, v0.y, v0.z}, b[3] = {e1.x, e1.y, e1.z}, c[3] = {e2.x, e2.y, e2.z};
+    for (int k = 0; k < 3; ++k) {
+        const float p1 = a[k] + b[k], p2 = a[k] + c[k];
+        const float l = fminf(fminf(a[k], p1), p2), h = fmaxf(fmaxf(a[k], p1), p2);
+        lo[k] = l - box_pad(l);
+        hi[k] = h + box_pad(h);
+    }
 }
 
-// Slab test of one child (lane c of the SoA node); boxes are padded at build time so the
-// fma form is conservative; tfar is widened by 4 ulp-ish as PBRT's robust test does.
-__device__ __forceinline__ float slab(float lx, float hx, float ly, float hy, float lz, float hz, f3 inv, f3 io,
-                                      float tmin, float tmax, bool& hit) {
-    float ax = __fmaf_rn(lx, inv.x, -io.x), bx = __fmaf_rn(hx, inv.x, -io.x);
-    float ay = __fmaf_rn(ly, inv.y, -io.y), by = __fmaf_rn(hy, inv.y, -io.y);
-    float az = __fmaf_rn(lz, inv.z, -io.z), bz = __fmaf_rn(hz, inv.z, -io.z);
-    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax)) * 1.0000004f;
-    hit = tn <= tf;
-    return tn;
+// Hit acceptance.  A Moller-Trumbore hit at t on triangle T counts only if t lies in the slab
+// interval [tn, tf] of T's padded box, with relative slack K = kSlabWiden:
+//     tn <= t*K,   t <= tf*K,   tn <= tf*K.
+// A node keeps a child box B iff max(tn_B, tmin) <= min(tf_B, best)*K (node_eval).  B contains
+// T's padded box and the slab distance is monotone in the plane coordinate, so tn_B <= tn and
+// tf_B >= tf: a box holding an acceptable hit with t <= best is never culled.  The closest hit
+// is therefore the (t, original index) minimum over the acceptable hits for ANY BVH and ANY
+// visiting order -- the oracle's binary median-split BVH and this BVH4 give the same answer.
+// Without the rule (round 1), a grazing ray could be accepted by Moller-Trumbore at a point
+// outside the triangle's own box (barycentric rounding at cos = 0.038), whose box the cull then
+// dropped or kept depending on which triangle had set `best` first -- a visiting-order, hence
+// wave-neighbour, dependence ("Closest-hit determinism").
+__device__ __forceinline__ bool tri_accept(const float4 A, const float4 E1, const float4 E2, f3 inv, f3 io, float t) {
+    float lo[3], hi[3];
+    tri_box_padded(mk(A.x, A.y, A.z), mk(E1.x, E1.y, E1.z), mk(E2.x, E2.y, E2.z), lo, hi);
+    const float ax = __fmaf_rn(lo[0], inv.x, -io.x), bx = __fmaf_rn(hi[0], inv.x, -io.x);
+    const float ay = __fmaf_rn(lo[1], inv.y, -io.y), by = __fmaf_rn(hi[1], inv.y, -io.y);
+    const float az = __fmaf_rn(lo[2], inv.z, -io.z), bz = __fmaf_rn(hi[2], inv.z, -io.z);
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tfk = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * kSlabWiden;
+    return tn <= t * kSlabWiden && t <= tfk && tn <= tfk;
 }
 
 __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
@@ -129,20 +134,10 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
 // back (both rare, separate branches — a pop that may read either memory compiles to a
 // slow flat load on every step).
 // The LDS depth is a template parameter (DEPTH): it trades LDS per workgroup against
-// occupancy per kernel (see pt_render.hip / pt_wavefront.hip).
-#ifndef PT_SPILL_DEPTH
-#define PT_SPILL_DEPTH 64
-#endif
-constexpr int kSpillDepth = PT_SPILL_DEPTH;  // spill + LDS hold a BVH4 path of depth > 20
-#ifndef PT_DUAL_STEP
-#define PT_DUAL_STEP 1  // one node AND one triangle per traversal step (see trav_step)
-#endif
-#ifndef PT_TRI_PER_STEP
-#define PT_TRI_PER_STEP 1
-#endif
-#ifndef PT_SKIP_LAST_SAMPLE
-#define PT_SKIP_LAST_SAMPLE 1  // no BSDF sample on a path's last segment (its ray is never traced)
-#endif
+// occupancy per kernel (see pt_render.hip / pt_wavefront.hip).  A traversal holds at most
+// 3 entries per BVH4 level, so DEPTH + kSpillDepth must be >= 3 * depth; pt_create rejects
+// deeper trees (kMaxBvhDepth).
+constexpr int kSpillDepth = 64;
 
 // ---- textures: devicePrograms.cu:62-73 (SRGB8ToLinear), :131-166 (GetTextureCoord,
 // SampleTextures), :518-543 (AlphaCutout); CreateTextures (OptixRenderer.cpp:562-612) sets up
@@ -203,28 +198,29 @@ __device__ __forceinline__ bool alpha_cut(const DevScene& S, int ti, int mi, flo
 }
 
 // ---- BVH4 traversal -----------------------------------------------------------------------
-// A per-lane state machine: one step is one inner node (4 slab tests, sorted push of the
-// far hits, descend) or one leaf (<= kLeafMax triangles).  traverse() loops it for one ray;
-// lane-refilling queue kernels (pt_wavefront.hip) interleave it with ray fetches.  Written
-// branch-reduced for 64-wide waves (PMC on the first version: ~16 % VALU lane utilisation,
-// SALU at 44 % of VALU from the per-push branches): the three pushes are unconditional
-// LDS stores with predicated stack-pointer increments and the triangle test is predicated
-// (same arithmetic and NaN behaviour as the oracle's tri_hit, without the early exits).
-// Closest hit is ordered by (t, original triangle index), so the result is independent of
-// BVH shape and visit order.
+// A per-lane state machine.  A lane carries one node (`cur`) and one leaf (`leaf`), and one
+// step visits the node (4 slab tests, sorted push of the far hits, descend) AND tests one
+// triangle of the leaf: a wave whose lanes are split between nodes and triangles executes
+// both halves anyway, so most lanes do useful work in both.  Written
+// branch-reduced for 64-wide waves: the three pushes are unconditional LDS stores with
+// predicated stack-pointer increments and the triangle test is predicated (same arithmetic
+// and NaN behaviour as the oracle's tri_hit, without the early exits).  Closest hit is
+// ordered by (t, original triangle index) over the acceptable hits (tri_accept), so the
+// result is independent of BVH shape and visit order.
 struct TravState {
     f3 o, d, inv, io;
     float tmin, best;
     int cur, sp, spc;  // current node/leaf, LDS stack depth, entries spilled
-    int leaf;          // PT_DUAL_STEP: leaf whose triangles are tested alongside node steps
+    int leaf;          // leaf whose triangles are tested alongside node steps
     int nx, ny, nz;    // byte offset (0 or 16) of the near slab plane per axis within the node
     bool any;          // any-hit ray (only read by kRayMixed traversals)
+    bool strict;       // re-trace: only acceptable hits are taken (trav_restart_strict)
     int path;          // wavefront extension rays: the path id, for the hit record
     Hit h;
 };
 
 // Ray kinds of a traversal (the ANY template argument): closest hit, any hit (shadow rays,
-// stop at the first accepted hit), or mixed queues where TravState::any decides per lane.
+// stop at the first hit), or mixed queues where TravState::any decides per lane.
 enum { kRayClosest = 0, kRayAny = 1, kRayMixed = 2 };
 
 __device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, float tmax) {
@@ -242,8 +238,14 @@ __device__ __forceinline__ void trav_init(TravState& s, f3 o, f3 d, float tmin, 
     s.spc = 0;
     s.leaf = kEmptyChild;
     s.any = false;
+    s.strict = false;
     s.h.tri = -1;
     s.h.orig = 0x7fffffff;
+}
+
+template <int ANY>
+__device__ __forceinline__ bool is_any(const TravState& s) {
+    return ANY == kRayAny || (ANY == kRayMixed && s.any);
 }
 
 // Moller-Trumbore; OptiX barycentric convention (u weights v1, v weights v2); closed
@@ -268,9 +270,8 @@ __device__ __forceinline__ bool tri_test(const float4 A, const float4 E1, const 
     return (det != 0.0f) & !(u < 0.0f || u > 1.0f) & !(v < 0.0f || u + v > 1.0f) & (t >= tmin && t <= tmax);
 }
 
-// Move the bottom (DEPTH / 2) LDS entries to the spill array (rare).  With the spill full
-// (BVH4 deeper than ~30 levels, never produced for real scenes) the oldest half is dropped
-// and counted in TravStats::overflow.
+// Move the bottom (DEPTH / 2) LDS entries to the spill array (rare).  pt_create bounds the
+// BVH depth so the spill never fills (kMaxBvhDepth); a full spill is still counted.
 template <int DEPTH, bool STATS>
 __device__ __forceinline__ void stack_spill(TravState& s, int* __restrict__ stk, int stride, int* spill,
                                          TravStats& ts) {
@@ -292,112 +293,9 @@ __device__ __forceinline__ void stack_refill(TravState& s, int* __restrict__ stk
     s.sp = (DEPTH / 2);
 }
 
-// Returns true when the ray is finished.  `spill` holds stack entries beyond the LDS
-// depth (never reached on the benchmark scenes; see the overflow counter).
-template <int ANY, bool STATS, int DEPTH, bool TEX>
-__device__ __forceinline__ bool trav_step_single(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
-                                          int* spill, TravStats& ts) {
-    if (s.cur >= 0) {
-        if (STATS) ts.nodes++;
-        const BNode4& n = S.nodes[s.cur];
-        const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
-        const int4 ch = n.child;
-        bool h0, h1, h2, h3;
-        float t0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, s.inv, s.io, s.tmin, s.best, h0);
-        float t1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, s.inv, s.io, s.tmin, s.best, h1);
-        float t2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, s.inv, s.io, s.tmin, s.best, h2);
-        float t3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, s.inv, s.io, s.tmin, s.best, h3);
-        const float inf = __int_as_float(0x7f800000);
-        int c0 = (h0 && ch.x != kEmptyChild) ? ch.x : kEmptyChild;
-        int c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
-        int c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
-        int c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
-        if (ANY != kRayAny || !PT_ANY_UNSORTED) {
-            t0 = c0 != kEmptyChild ? t0 : inf;
-            t1 = c1 != kEmptyChild ? t1 : inf;
-            t2 = c2 != kEmptyChild ? t2 : inf;
-            t3 = c3 != kEmptyChild ? t3 : inf;
-            // sort ascending (optimal 4-network); misses sink to the end with t = inf
-            cswap(t0, c0, t1, c1);
-            cswap(t2, c2, t3, c3);
-            cswap(t0, c0, t2, c2);
-            cswap(t1, c1, t3, c3);
-            cswap(t1, c1, t2, c2);
-        }  // any-hit: visit order does not change the answer, skip the sort
-        // push the farther hits (far first), continue with the nearest
-        if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
-        {  // unconditional stores, predicated sp: an empty child's store lands in the slot
-           // the next valid one overwrites
-            int sp = s.sp;
-            stk[sp * stride] = c3;
-            sp += c3 != kEmptyChild;
-            stk[sp * stride] = c2;
-            sp += c2 != kEmptyChild;
-            stk[sp * stride] = c1;
-            sp += c1 != kEmptyChild;
-            s.sp = sp;
-        }
-        if (c0 != kEmptyChild) {
-            s.cur = c0;
-            return false;
-        }
-    } else {
-        const int first = leaf_first(s.cur), cnt = leaf_count(s.cur);
-#if PT_TRI_PER_STEP
-        // one triangle per step: a lane in a leaf costs the wave one triangle test per
-        // iteration instead of holding node lanes for the whole leaf
-        const int ti = first;
-        {
-#else
-        for (int k = 0; k < cnt; ++k) {
-            const int ti = first + k;
-#endif
-            if (STATS) ts.tris++;
-            const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
-            float t, u, v;
-            bool bk;
-            bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
-            if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
-            const int oi = __float_as_int(A.w);
-            if (ANY == kRayAny || (ANY == kRayMixed && s.any)) {
-                if (hit) {
-                    s.h.tri = ti;
-                    s.h.orig = oi;
-                    return true;
-                }
-            } else {
-                const bool take = hit && (t < s.best || oi < s.h.orig);
-                s.best = take ? t : s.best;
-                s.h.t = take ? t : s.h.t;
-                s.h.u = take ? u : s.h.u;
-                s.h.v = take ? v : s.h.v;
-                s.h.back = take ? bk : s.h.back;
-                s.h.tri = take ? ti : s.h.tri;
-                s.h.orig = take ? oi : s.h.orig;
-            }
-        }
-#if PT_TRI_PER_STEP
-        if (cnt > 1) {
-            s.cur = ~(((first + 1) << 3) | (cnt - 2));  // rest of the leaf
-            return false;
-        }
-#endif
-    }
-    if (s.sp == 0) {
-        if (s.spc == 0) return true;
-        stack_refill<DEPTH>(s, stk, stride, spill);
-    }
-    --s.sp;
-    s.cur = stk[s.sp * stride];
-    return false;
-}
-
-#ifndef PT_NODE_SIGNSEL
-#define PT_NODE_SIGNSEL 1
-#endif
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
-// The six sign-selected planes and the child links of one node, as loaded (PT_NODE_SIGNSEL).
+// The six sign-selected planes and the child links of one node, as loaded.
 struct NodeLoad {
     float4 ax, bx, ay, by, az, bz;
     int4 ch;
@@ -422,11 +320,11 @@ __device__ __forceinline__ NodeLoad node_load(const DevScene& S, const TravState
 }
 
 // Slab test of the four children of a loaded node, hits as (t_near, child) with misses and
-// empty slots as kEmptyChild.  The ray's direction signs picked the near and far plane of
-// every axis at load time (per-lane byte offsets into the node), so each child needs no
-// min/max per axis, and the plane distances are two children per packed v_pk_fma.  The
-// planes are the same ones min/max would choose (fma is monotone in the plane coordinate),
-// so the result equals slab()'s.
+// empty slots as (inf, kEmptyChild).  The ray's direction signs picked the near and far plane
+// of every axis at load time (per-lane byte offsets into the node), so each child needs no
+// min/max per axis, and the plane distances are two children per packed v_pk_fma.  The planes
+// are the ones min/max would choose (fma is monotone in the plane coordinate), so the slab
+// distances equal tri_accept's and the oracle's box_hit's bit for bit.
 __device__ __forceinline__ void node_eval(const NodeLoad& n, const TravState& s, float& t0, float& t1, float& t2,
                                           float& t3, int& c0, int& c1, int& c2, int& c3) {
     bool h0, h1, h2, h3;
@@ -453,13 +351,13 @@ __device__ __forceinline__ void node_eval(const NodeLoad& n, const TravState& s,
     t3 = fmaxf(fmaxf(nx23.y, ny23.y), fmaxf(nz23.y, tmin));
     pt_f2 f01 = {fminf(fminf(fx01.x, fy01.x), fminf(fz01.x, tmax)), fminf(fminf(fx01.y, fy01.y), fminf(fz01.y, tmax))};
     pt_f2 f23 = {fminf(fminf(fx23.x, fy23.x), fminf(fz23.x, tmax)), fminf(fminf(fx23.y, fy23.y), fminf(fz23.y, tmax))};
-    f01 = f01 * pt_f2{1.0000004f, 1.0000004f};
-    f23 = f23 * pt_f2{1.0000004f, 1.0000004f};
+    f01 = f01 * pt_f2{kSlabWiden, kSlabWiden};
+    f23 = f23 * pt_f2{kSlabWiden, kSlabWiden};
     h0 = t0 <= f01.x;
     h1 = t1 <= f01.y;
     h2 = t2 <= f23.x;
     h3 = t3 <= f23.y;
-    // empty slots hold inverted boxes (pt_build.hip k_collapse): they never hit
+    // empty slots hold inverted boxes (pt_build.hip k_collapse_sah): they never hit
     const float inf = __int_as_float(0x7f800000);
     t0 = h0 ? t0 : inf;
     t1 = h1 ? t1 : inf;
@@ -471,33 +369,10 @@ __device__ __forceinline__ void node_eval(const NodeLoad& n, const TravState& s,
     c3 = h3 ? ch.w : kEmptyChild;
 }
 
-// Slab test of the four children of node `ni` (PT_NODE_SIGNSEL: node_load + node_eval).
-__device__ __forceinline__ void node_test(const DevScene& S, const TravState& s, int ni, float& t0, float& t1,
-                                          float& t2, float& t3, int& c0, int& c1, int& c2, int& c3) {
-#if PT_NODE_SIGNSEL
-    node_eval(node_load(S, s, ni), s, t0, t1, t2, t3, c0, c1, c2, c3);
-#else
-    bool h0, h1, h2, h3;
-    const BNode4& n = S.nodes[ni];
-    const int4 ch = n.child;
-    const float4 lx = n.lox, hx = n.hix, ly = n.loy, hy = n.hiy, lz = n.loz, hz = n.hiz;
-    t0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, s.inv, s.io, s.tmin, s.best, h0);
-    t1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, s.inv, s.io, s.tmin, s.best, h1);
-    t2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, s.inv, s.io, s.tmin, s.best, h2);
-    t3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, s.inv, s.io, s.tmin, s.best, h3);
-    c0 = (h0 && ch.x != kEmptyChild) ? ch.x : kEmptyChild;
-    c1 = (h1 && ch.y != kEmptyChild) ? ch.y : kEmptyChild;
-    c2 = (h2 && ch.z != kEmptyChild) ? ch.z : kEmptyChild;
-    c3 = (h3 && ch.w != kEmptyChild) ? ch.w : kEmptyChild;
-    const float inf = __int_as_float(0x7f800000);
-    t0 = c0 != kEmptyChild ? t0 : inf;
-    t1 = c1 != kEmptyChild ? t1 : inf;
-    t2 = c2 != kEmptyChild ? t2 : inf;
-    t3 = c3 != kEmptyChild ? t3 : inf;
-#endif
-}
-
 // Test one triangle of the leaf s.leaf and advance it; true when an any-hit ray is done.
+// Closest-hit lanes take a hit by the (t, original index) order; in strict mode
+// (trav_restart_strict) only acceptable hits count.  Any-hit lanes stop at the first hit and
+// record only h.tri (the shadow queue carries the path and contribution in h's other fields).
 template <int ANY, bool STATS, bool TEX>
 __device__ __forceinline__ bool leaf_tri_eval(const DevScene& S, TravState& s, TravStats& ts, const float4 A,
                                               const float4 E1, const float4 E2) {
@@ -508,16 +383,15 @@ __device__ __forceinline__ bool leaf_tri_eval(const DevScene& S, TravState& s, T
     bool bk;
     bool hit = tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
     if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
+    if (s.strict && hit) hit = tri_accept(A, E1, E2, s.inv, s.io, t);  // rare re-trace lanes only
     const int oi = __float_as_int(A.w);
     s.leaf = cnt > 1 ? ~(((first + 1) << 3) | (cnt - 2)) : kEmptyChild;  // rest of the leaf
-    if (ANY == kRayAny || (ANY == kRayMixed && s.any)) {
+    if (is_any<ANY>(s)) {
         if (hit) {
             s.h.tri = ti;
-            s.h.orig = oi;
             return true;
         }
     } else {
-        // closest hit ordered by (t, original index): independent of the visiting order
         const bool take = hit && (t < s.best || oi < s.h.orig);
         s.best = take ? t : s.best;
         s.h.t = take ? t : s.h.t;
@@ -546,21 +420,14 @@ __device__ __forceinline__ void stack_pop(TravState& s, int* __restrict__ stk, i
     s.sp = max(sp, 0);
 }
 
-// One traversal step; true when the ray is finished.  `spill` holds stack entries beyond
-// the LDS depth (never reached on the benchmark scenes; see the overflow counter).
-//
-// PT_DUAL_STEP: a lane carries a node (s.cur) and a leaf (s.leaf) at once, and one step
-// tests one triangle of the leaf AND visits the node.  A wave whose lanes are split between
-// nodes and triangles executes both halves of the step anyway; here most lanes do useful
-// work in both, so a ray finishes in ~max(nodes, triangles) steps instead of their sum.
-// Leaves are therefore tested out of front-to-back order, which the (t, index) closest-hit
-// rule makes harmless; culling stays conservative (best only shrinks).
-// `tri_ok` (wave-uniform) lets the caller postpone the triangle half of the step until enough
-// lanes hold a leaf (trace_slice); lanes keep traversing nodes meanwhile.
+// One traversal step (one triangle of the pending leaf AND one node); true when the ray is
+// finished.  Leaves are tested out of front-to-back order, which the (t, index) closest-hit
+// rule makes harmless; culling stays conservative (best only shrinks).  `tri_ok`
+// (wave-uniform) lets the caller postpone the triangle half of the step until enough lanes
+// hold a leaf (trace_range); lanes keep traversing nodes meanwhile.
 template <int ANY, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                           int* spill, TravStats& ts, bool tri_ok = true) {
-#if PT_DUAL_STEP
     // (issuing the triangle and node loads before either test overlaps their round trips but
     // needs 116 VGPRs, one wave per SIMD fewer: -1.5 % Lambert, -22 % Dielectric)
     if (tri_ok && s.leaf != kEmptyChild) {
@@ -570,18 +437,17 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         if (STATS) ts.nodes++;
         float t0, t1, t2, t3;
         int c0, c1, c2, c3;
-        node_test(S, s, s.cur, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
-        if ((ANY != kRayAny || !PT_ANY_UNSORTED) && PT_CHILD_SORT > 0) {
+        node_eval(node_load(S, s, s.cur), s, t0, t1, t2, t3, c0, c1, c2, c3);  // misses: t = inf
+        if (ANY != kRayAny) {  // nearest first; an any-hit ray's answer does not depend on order
             cswap(t0, c0, t1, c1);
             cswap(t2, c2, t3, c3);
             cswap(t0, c0, t2, c2);  // c0 nearest
-            if (PT_CHILD_SORT > 1) {
-                cswap(t1, c1, t3, c3);
-                cswap(t1, c1, t2, c2);
-            }
+            cswap(t1, c1, t3, c3);
+            cswap(t1, c1, t2, c2);
         }
         if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
-        {
+        {  // unconditional stores, predicated sp: an empty child's store lands in the slot the
+           // next valid one overwrites
             int sp = s.sp;
             stk[sp * stride] = c3;
             sp += c3 != kEmptyChild;
@@ -600,9 +466,39 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
         stack_pop<DEPTH>(s, stk, stride, spill);
     }
     return s.cur == kEmptyChild && s.leaf == kEmptyChild;
-#else
-    return trav_step_single<ANY, STATS, DEPTH, TEX>(S, s, stk, stride, spill, ts);
-#endif
+}
+
+// A finished traversal's answer stands unless its hit is not acceptable (tri_accept) -- then
+// the ray is traced again in strict mode.  If the final hit is acceptable it IS the minimum
+// over the acceptable hits: every acceptable hit ordered before it had t <= best throughout,
+// so its boxes were never culled and it was tested and taken.  The check recomputes the hit
+// (same arithmetic, same t) from the triangle record; it runs once per finished ray.
+template <bool TEX>
+__device__ __forceinline__ bool trav_result_ok(const DevScene& S, const TravState& s) {
+    if (s.strict || s.h.tri < 0) return true;
+    const int ti = s.h.tri;
+    const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+    float t, u, v;
+    bool bk;
+    (void)tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
+    return tri_accept(A, E1, E2, s.inv, s.io, t);
+}
+
+// Trace the ray again from the root, taking acceptable hits only.  Closest-hit lanes restart
+// from tmax_closest; any-hit lanes keep their tmax (best never shrinks for them) and their
+// carried fields.
+template <int ANY>
+__device__ __forceinline__ void trav_restart_strict(TravState& s, float tmax_closest) {
+    s.cur = 0;
+    s.sp = 0;
+    s.spc = 0;
+    s.leaf = kEmptyChild;
+    s.strict = true;
+    s.h.tri = -1;
+    if (!is_any<ANY>(s)) {
+        s.best = tmax_closest;
+        s.h.orig = 0x7fffffff;
+    }
 }
 
 // Whole traversal of one ray (megakernel, k_trace).
@@ -614,7 +510,12 @@ __device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tm
     trav_init(s, o, d, tmin, tmax);
     if (S.ntri > 0) {
         int spill[kSpillDepth];
-        while (!trav_step<ANY, STATS, DEPTH, TEX>(S, s, stk, stride, spill, ts)) {
+        while (true) {
+            while (!trav_step<ANY, STATS, DEPTH, TEX>(S, s, stk, stride, spill, ts)) {
+            }
+            if (trav_result_ok<TEX>(S, s)) break;
+            if (STATS) ts.retrace++;
+            trav_restart_strict<ANY>(s, tmax);
         }
     }
     h = s.h;
@@ -802,7 +703,7 @@ __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch&
     BSample bs;
     // the last segment's sampled direction is never traced (SamplePath's loop test, :646):
     // skipping the sample leaves every traced value unchanged
-    if (PT_SKIP_LAST_SAMPLE && p.bounce >= L.max_bounces) {
+    if (p.bounce >= L.max_bounces) {
         p.end = true;
         return;
     }

@@ -39,11 +39,13 @@ __device__ __forceinline__ void flush_stats(const DevLaunch& L, uint32_t segs, c
         unsigned long long c = wave_sum((unsigned long long)ts.tris);
         unsigned long long d = wave_sum((unsigned long long)ts.rays);
         unsigned long long e = wave_sum((unsigned long long)ts.overflow);
+        unsigned long long g = wave_sum((unsigned long long)ts.retrace);
         if (lane == 0 && L.counters) {
             atomicAdd(&L.counters[1], b);
             atomicAdd(&L.counters[2], c);
             atomicAdd(&L.counters[3], d);
             atomicAdd(&L.counters[4], e);
+            atomicAdd(&L.counters[8], g);
         }
     }
     if (lane == 0 && L.counters) atomicAdd(&L.counters[0], a);
@@ -103,7 +105,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(DevScene S, const float* rays,
     int* stk = stack + threadIdx.x;
     bool hit = any_hit ? traverse<true, false, kStack, TEX>(S, o, d, r[6], r[7], h, stk, kBlock, ts)
                        : traverse<false, false, kStack, TEX>(S, o, d, r[6], r[7], h, stk, kBlock, ts);
-    prim[i] = hit ? h.orig : -1;
+    // any-hit: the occluder's original index (an any-hit traversal records only its leaf slot)
+    prim[i] = hit ? (any_hit ? __float_as_int(S.isect[3 * h.tri].w) : h.orig) : -1;
     th[i] = hit && !any_hit ? h.t : 0.0f;
     uh[i] = hit && !any_hit ? h.u : 0.0f;
     vh[i] = hit && !any_hit ? h.v : 0.0f;

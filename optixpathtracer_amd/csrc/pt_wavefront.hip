@@ -46,28 +46,38 @@ constexpr int kStack = PT_WF_STACK;
 #define PT_WF_WAVES 1
 #endif
 constexpr int kMissTri = -1;
-#ifndef PT_SHADOW_CARRY
-#define PT_SHADOW_CARRY 1  // shadow rays carry path + contribution in the hit record (k_trace_pair)
-#endif
-#ifndef PT_HIT_PATH
-#define PT_HIT_PATH 1  // hit records carry the path id instead of t (shading needs no ray_o read)
-#endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// Hit record of a finished extension ray: (t | path, u, v, tri | back << 31), or a miss.
-// The shading kernels reconstruct the surface from (tri, u, v) and never read t, so with
-// PT_HIT_PATH the first word carries the path id and they skip the ray_o read.
+// Hit record of a finished extension ray: (path, u, v, tri | back << 31), or a miss.  The
+// shading kernels reconstruct the surface from (tri, u, v) and never read t, so the first word
+// carries the path id and they skip the ray_o read.
 __device__ __forceinline__ float4 hit_record(const Hit& h, int path) {
-    const float x = PT_HIT_PATH ? __int_as_float(path) : h.t;
+    const float x = __int_as_float(path);
     return h.tri >= 0 ? make_float4(x, h.u, h.v, __int_as_float(h.tri | (h.back ? (int)0x80000000 : 0)))
-                      : make_float4(PT_HIT_PATH ? x : 0.0f, 0.0f, 0.0f, __int_as_float(kMissTri));
+                      : make_float4(x, 0.0f, 0.0f, __int_as_float(kMissTri));
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// Traversal statistics of a wave into the renderer's counters ([1] nodes, [2] triangle tests,
+// [3] rays, [4] stack overflows, [8] strict re-traces).
+template <bool STATS>
+__device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, const TravStats& ts) {
+    if (!STATS || !counters) return;
+    const unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
+    const unsigned long long e = wave_sum_u64(ts.overflow), r = wave_sum_u64(ts.retrace);
+    if (lane_id() == 0) {
+        atomicAdd(&counters[1], a);
+        atomicAdd(&counters[2], c);
+        atomicAdd(&counters[3], d);
+        atomicAdd(&counters[4], e);
+        atomicAdd(&counters[8], r);
+    }
 }
 
 // Per-bounce counters: queue length and shadow-queue length, each on its own 128-B line
@@ -105,9 +115,6 @@ constexpr int shf_waves(int mode) { return (mode == 1 || mode == 3) /*Lambert, D
 #define PT_SHB_BLOCK 1024
 #endif
 constexpr int kBlockShB = PT_SHB_BLOCK;
-#ifndef PT_SHB_BUCKET
-#define PT_SHB_BUCKET 1  // k_shade_b groups its compacted items by material (conductor coin)
-#endif
 
 // Block-wide compaction: every thread of the block calls this (uniform control flow);
 // threads with pred get consecutive slots.  `lds` is kWavesSh + 1 ints of shared memory
@@ -169,99 +176,75 @@ __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
     end = min(n, first + per);
 }
 
-// Queue records are streamed once per launch; PT_NT_QUEUE marks those loads and stores
-// non-temporal so they do not evict BVH / triangle lines from L2.
-#ifndef PT_NT_QUEUE
-#define PT_NT_QUEUE 0
-#endif
 typedef float pt_v4f __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ldq(const float4* p) {
-#if PT_NT_QUEUE
-    const pt_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pt_v4f*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ void stq(float4* p, float4 v) {
-#if PT_NT_QUEUE
-    __builtin_nontemporal_store(pt_v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<pt_v4f*>(p));
-#else
-    *p = v;
-#endif
-}
-
 // k_shade_fused (the memory-bound kernel of a fused-mode frame, ≈ 66 % of HBM peak) streams
-// its queue records once: non-temporal loads (1) and stores (1, 2) keep them from evicting the
-// triangle and material lines its gathers reuse.  Lambert +1.7 %, Dielectric and Conductor
-// +0.4 %.
-#ifndef PT_NT_SHADE
-#define PT_NT_SHADE 1
-#endif
-#ifndef PT_NT_BETA
-#define PT_NT_BETA 1  // also the path state read-modify-write (+0.3 % Lambert and Conductor, 4 rounds)
-#endif
+// its queue records and the path state once: non-temporal loads and stores keep them from
+// evicting the triangle and material lines its gathers reuse.  Lambert +2 %, Dielectric and
+// Conductor +0.4 %.  (The same hint on the trace kernels' queues: ±0.5 %, not
+// used -- they are not memory-bound.)
 __device__ __forceinline__ float4 ldqs(const float4* p) {
-#if PT_NT_SHADE == 1
     const pt_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pt_v4f*>(p));
     return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
 }
 __device__ __forceinline__ void stqs(float4* p, float4 v) {
-#if PT_NT_SHADE
     __builtin_nontemporal_store(pt_v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<pt_v4f*>(p));
-#else
-    *p = v;
-#endif
 }
 
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
-// for ray ri, `finish(ri, state)` consumes a finished ray.
+// for ray ri, `finish(ri, state)` consumes a finished ray.  A lane whose traversal ends parks
+// (`done`) until enough lanes are idle; then the wave runs one batch block that checks the
+// parked results (trav_result_ok: a rare unacceptable hit sends its lane back into a strict
+// re-trace instead), finishes them and refills the idle lanes with the next rays of the
+// slice.  Closest-hit lanes trace in [0, tmax_closest].
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
-__device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TravStats& ts,
-                                            Fetch fetch, Finish finish) {
+__device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, float tmax_closest, int* stk,
+                                            TravStats& ts, Fetch fetch, Finish finish) {
     int spill[kSpillDepth];
     TravState st;
     int ri = -1;
+    bool done = false;
     // the slice bounds are wave-uniform: keeping them (and the refill bookkeeping) in SGPRs
     // makes the per-step refill test scalar work (it was VALU, with an f64 min from the
     // unsigned popcount; ±0.3 %)
     next = __builtin_amdgcn_readfirstlane(next);
     end = __builtin_amdgcn_readfirstlane(end);
     while (true) {
-        const bool need = ri < 0;
-        unsigned long long m = __ballot(need ? 1 : 0);
-        // refill once enough lanes idle (the refill block costs the wave as much as a step)
-        if ((int)__popcll(m) < kRefillMin && next < end) m = 0;  // (< kRefillMin lanes: m != ~0)
-        const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (need && m && next + pre < end) {
-            ri = next + pre;
-            fetch(ri, st);
-            if (STATS) ts.rays++;
-            if (S.ntri <= 0) {  // empty scene: no BVH root, every ray misses
-                finish(ri, st);
-                ri = -1;
+        // batch block once enough lanes idle (it costs the wave about as much as a step), and
+        // at every step once the slice is drained
+        if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
+            if (done) {
+                if (trav_result_ok<TEX>(S, st)) {
+                    finish(ri, st);
+                    ri = -1;
+                } else {
+                    trav_restart_strict<ANY>(st, tmax_closest);
+                    if (STATS) ts.retrace++;
+                }
+                done = false;
             }
+            const unsigned long long m = __ballot(ri < 0);
+            const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (ri < 0 && next + pre < end) {
+                ri = next + pre;
+                fetch(ri, st);
+                if (STATS) ts.rays++;
+                done = S.ntri <= 0;  // empty scene: no BVH root, every ray misses
+            }
+            next = min(next + (int)__popcll(m), end);
         }
-        next = min(next + (int)__popcll(m), end);
-        const unsigned long long act = __ballot(ri >= 0 ? 1 : 0);
-        if (!act) break;
-#if PT_DUAL_STEP && PT_TRI_BATCH > 0
+        const bool active = ri >= 0 && !done;
+        const unsigned long long act = __ballot(active);
+        if (!act) {
+            if (!__ballot(ri >= 0)) break;
+            continue;  // only parked lanes left: the next batch block finishes them
+        }
         // postponed leaves: run the triangle half of the step once enough lanes hold a leaf,
         // or when too few lanes have a node left to visit (then the leaves are the work)
         const int n_act = __popcll(act);
-        const int n_leaf = __popcll(__ballot(ri >= 0 && st.leaf != kEmptyChild ? 1 : 0));
-        const int n_node = __popcll(__ballot(ri >= 0 && st.cur >= 0 ? 1 : 0));
+        const int n_leaf = __popcll(__ballot(active && st.leaf != kEmptyChild));
+        const int n_node = __popcll(__ballot(active && st.cur >= 0));
         const bool tri_ok = n_leaf >= min(PT_TRI_BATCH, n_act) || 2 * n_node < n_act;
-#else
-        const bool tri_ok = true;
-#endif
-        if (ri >= 0 && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts, tri_ok)) {
-            finish(ri, st);
-            ri = -1;
-        }
+        if (active && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts, tri_ok)) done = true;
     }
 }
 
@@ -270,7 +253,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
                                             Finish finish) {
     int next, end;
     wave_slice(n, next, end);
-    trace_range<ANY, STATS, TEX>(S, next, end, stk, ts, fetch, finish);
+    trace_range<ANY, STATS, TEX>(S, next, end, 100.0f, stk, ts, fetch, finish);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -291,30 +274,21 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
     trace_slice<kRayClosest, STATS, TEX>(
         S, n_trace, stk, ts,
         [&](int ri, TravState& st) {
-            const float4 a = ldq(ro + ri), c = ldq(rd + ri);
+            const float4 a = ro[ri], c = rd[ri];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
             st.path = __float_as_int(a.w);
         },
         [&](int ri, const TravState& st) {
             // copy k of a bounce-0 ray is path st.path + k * n_trace (queue 0 is in path order)
             for (int k = 0; k < dup; ++k)
-                stq(W.hit + ri + (size_t)k * n_trace, hit_record(st.h, st.path + k * n_trace));
+                W.hit[ri + (size_t)k * n_trace] = hit_record(st.h, st.path + k * n_trace);
         });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n);        // path segments
         atomicAdd(&counters[6], (unsigned long long)n_trace);  // rays traced by the timed trace kernels
         atomicAdd(&counters[7], 32ull * (unsigned long long)n_trace + 16ull * (unsigned long long)n);  // bytes
     }
-    if (STATS && counters) {
-        unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
-        unsigned long long e = wave_sum_u64(ts.overflow);
-        if (lane_id() == 0) {
-            atomicAdd(&counters[1], a);
-            atomicAdd(&counters[2], c);
-            atomicAdd(&counters[3], d);
-            atomicAdd(&counters[4], e);
-        }
-    }
+    flush_trav_stats<STATS>(counters, ts);
 }
 
 __device__ __forceinline__ Hit decode_hit(float4 hv) {
@@ -390,7 +364,6 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
-    const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
@@ -405,18 +378,14 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
         int path = 0;
         if (valid) {
             const float4 hv = ldqs(W.hit + i);
-            path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
+            path = __float_as_int(hv.x);
             const Hit h = decode_hit(hv);
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
                 const float4 c = ldqs(rd + i);
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
-                #if PT_NT_BETA
                 float4 bv = ldqs(W.beta + path);
-#else
-                float4 bv = W.beta[path];
-#endif
                 uint32_t seed = __float_as_uint(bv.w);
                 f3 beta = mk(bv.x, bv.y, bv.z);
                 const bool conductor = rnd(seed) < sf.metallic;  // :400
@@ -451,14 +420,10 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 }
                 BSample bs;
                 // the last bounce's sampled direction is never traced (SamplePath :646)
-                if ((!PT_SKIP_LAST_SAMPLE || b + 1 < L.max_bounces) &&
+                if (b + 1 < L.max_bounces &&
                     bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
                     emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
-                    #if PT_NT_BETA
                     stqs(W.beta + path, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
-#else
-                    W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
-#endif
                 }
             }
         }
@@ -491,74 +456,52 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
     int* stk = stack + threadIdx.x;
     TravStats ts;
     auto fetch = [&](int i, TravState& st) {
-#ifdef PT_EXP_FAKEFETCH  // timing experiment only: ray records from an L2-resident window (wrong images)
-            i = i < n_ext ? (i % PT_EXP_FAKEFETCH) : n_ext + ((i - n_ext) % PT_EXP_FAKEFETCH);
-#endif
-            if (i < n_ext) {
-                const float4 a = ldq(ro + i), c = ldq(rd + i);
-                trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
-                st.path = __float_as_int(a.w);
-            } else {
-                const int j = i - n_ext;
-                const float4 a = ldq(W.sh_o + j), c = ldq(W.sh_d + j);
-                trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
-                st.any = true;
-#if PT_SHADOW_CARRY
-                // an any-hit traversal only writes h.tri / h.orig, and only when occluded: the
-                // record's free fields carry the path and the contribution to finish()
-                const float4 k = ldq(W.sh_c + j);
-                st.h.orig = __float_as_int(a.w);
-                st.h.t = k.x;
-                st.h.u = k.y;
-                st.h.v = k.z;
-#endif
-            }
-        };
+        if (i < n_ext) {
+            const float4 a = ro[i], c = rd[i];
+            trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
+            st.path = __float_as_int(a.w);
+        } else {
+            const int j = i - n_ext;
+            const float4 a = W.sh_o[j], c = W.sh_d[j];
+            trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
+            st.any = true;
+            // an any-hit traversal only writes h.tri: the record's other fields carry the path
+            // and the contribution to finish()
+            const float4 k = W.sh_c[j];
+            st.h.orig = __float_as_int(a.w);
+            st.h.t = k.x;
+            st.h.u = k.y;
+            st.h.v = k.z;
+        }
+    };
     auto finish = [&](int i, const TravState& st) {
-            const Hit& h = st.h;
-            if (i < n_ext) {
-                stq(W.hit + i, hit_record(h, st.path));
-            } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
-#if PT_SHADOW_CARRY
-                const int path = h.orig;
-                const float4 k = make_float4(h.t, h.u, h.v, 0.0f);
-#else
-                const int j = i - n_ext;
-                const int path = __float_as_int(W.sh_o[j].w);
-                const float4 k = ldq(W.sh_c + j);
-#endif
-                const float4 l = W.L[path];
-                W.L[path] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
-            }
-        };
+        const Hit& h = st.h;
+        if (i < n_ext) {
+            W.hit[i] = hit_record(h, st.path);
+        } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+            const int path = h.orig;
+            const float4 l = W.L[path];
+            W.L[path] = make_float4(l.x + h.t, l.y + h.u, l.z + h.v, 0.0f);
+        }
+    };
     // The queue is [extension rays | shadow rays] in contiguous wave slices, so all but one wave
     // trace a single ray kind; a mixed-kind loop serves both (per-kind loops in one kernel and
     // per-wave shares of both kinds were slower).
     int first, end;
     wave_slice(n_ext + n_sh, first, end);
-    trace_range<kRayMixed, STATS, TEX>(S, first, end, stk, ts, fetch, finish);
+    trace_range<kRayMixed, STATS, TEX>(S, first, end, 100.0f, stk, ts, fetch, finish);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
         atomicAdd(&counters[6], (unsigned long long)(n_ext + n_sh));  // rays of timed trace kernels
         atomicAdd(&counters[7], 48ull * (unsigned long long)(n_ext + n_sh));  // their queue bytes
     }
-    if (STATS && counters) {
-        unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
-        unsigned long long e = wave_sum_u64(ts.overflow);
-        if (lane_id() == 0) {
-            atomicAdd(&counters[1], a);
-            atomicAdd(&counters[2], c);
-            atomicAdd(&counters[3], d);
-            atomicAdd(&counters[4], e);
-        }
-    }
+    flush_trav_stats<STATS>(counters, ts);
 }
 
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
-    const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     __shared__ int lds_sh[kWavesSh + 1];
     if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
@@ -571,7 +514,7 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
         int path = 0;
         if (valid) {
             const float4 hv = W.hit[i];
-            path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
+            path = __float_as_int(hv.x);
             const Hit h = decode_hit(hv);
             if (h.tri >= 0) {
                 const float4 c = rd[i];
@@ -659,7 +602,6 @@ template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     constexpr int kW = kBlockShB / 64;
     const int n = *cnt(W, b, kQueue);
-    const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
@@ -671,11 +613,11 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
     bool hit = false, nee = false, conductor = false;
     if (i < n) {
         const float4 hv = W.hit[i];
-        const int path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[i].w);
+        const int path = __float_as_int(hv.x);
         hit = __float_as_int(hv.w) != kMissTri;
         if (hit) {
             const int aux = W.aux[path];
-            conductor = PT_SHB_BUCKET && (aux & 1);
+            conductor = aux & 1;
             nee = L.n_lights > 0 && W.vis[vis0 ? vis0_index(L, path, aux >> 1) : path];
         }
     }
@@ -683,14 +625,14 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
     const int s_nee = block_bucket_scan<kW>(nee, conductor, lds_scan_a, n_nee);
     if (nee) lds_nee[s_nee] = i;
     // the last bounce's sampled direction is never traced (SamplePath :646): no sample items
-    const bool smp = hit && (!PT_SKIP_LAST_SAMPLE || b + 1 < L.max_bounces);
+    const bool smp = hit && b + 1 < L.max_bounces;
     const int s_smp = block_bucket_scan<kW>(smp, conductor, lds_scan_b, n_smp);
     if (smp) lds_smp[s_smp] = i;
     __syncthreads();
     if ((int)threadIdx.x < n_nee) {  // NEE: the light is visible (devicePrograms.cu:446-472)
         const int j = lds_nee[threadIdx.x];
         const float4 hv = W.hit[j], c = rd[j];
-        const int path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[j].w);
+        const int path = __float_as_int(hv.x);
         const Hit h = decode_hit(hv);
         SurfaceHit sf;
         reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
@@ -722,7 +664,7 @@ __global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, 
     if ((int)threadIdx.x < n_smp) {  // BSDF sample + continuation (devicePrograms.cu:474-509)
         const int j = lds_smp[threadIdx.x];
         const float4 hv = W.hit[j], c = rd[j];
-        path = PT_HIT_PATH ? __float_as_int(hv.x) : __float_as_int(ro[j].w);
+        path = __float_as_int(hv.x);
         const Hit h = decode_hit(hv);
         d = mk(c.x, c.y, c.z);
         SurfaceHit sf;

@@ -249,6 +249,16 @@ class OptixRenderer:
                                      1 if any_hit else 0), "pt_trace_rays")
         return prim, t, u, v, back
 
+    def bvh_arrays(self):
+        """(nodes, triangles): the BVH4 node array as (bvh_nodes, 32) uint32 words and the
+        leaf-ordered triangle records as (triangles, 12) uint32 words (pt_bvh_download)."""
+        st = self.stats()
+        nodes = np.zeros((st["bvh_nodes"], 32), np.uint32)
+        tris = np.zeros((st["triangles"], 12), np.uint32)
+        check(self.lib.pt_bvh_download(self.h, nodes.ctypes.data, nodes.nbytes, tris.ctypes.data, tris.nbytes),
+              "pt_bvh_download")
+        return nodes, tris
+
     def close(self) -> None:
         if getattr(self, "h", None):
             self.lib.pt_destroy(self.h)

@@ -975,12 +975,45 @@ static int alpha_cut(const orc_scene* s, int t, float u, float v) {
     return c[3] < 0.9f;
 }
 
+/* ---- Closest-hit rule shared with the kernels (pt_device.h tri_accept / node_eval) ------
+ * OptiX's closest hit comes from closed code (devicePrograms.cu:243-260); this restatement
+ * defines it as the (t, global index) minimum over the ACCEPTABLE Moller-Trumbore hits: the
+ * hit's t must lie in the slab interval of the triangle's own padded box, with relative slack
+ * K = 1 + 2^-12.  The box uses the vertices as the hit test sees them (v0, v0 + e1, v0 + e2);
+ * slab distances are fmaf(plane, inv, -o*inv) with inv = 1/d (a zero component -> +-1e30).
+ * Every BVH box below is a union of these boxes, and the box cull keeps a box iff
+ * max(tn, tmin) <= min(tf, best) * K, so no box holding an acceptable hit with t <= best is
+ * culled: the answer is the same for any BVH and any visiting order (the kernels' BVH4 and
+ * this binary median split agree bit for bit).  Without the rule a grazing ray could be
+ * accepted at a point outside the triangle's own box and the answer depended on which
+ * triangle set `best` first (one trace in 62 M of the config-5 band). */
+static const float kSlabWiden = 1.000244140625f;
+static inline float ray_inv(float d) { return d != 0.0f ? 1.0f / d : copysignf(1e30f, d); }
+static inline float box_pad(float x) { return fabsf(x) * 9.5367431640625e-7f + 1e-6f; }
 static void tri_bounds(const orc_scene* s, int t, float lo[3], float hi[3]) {
-    for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+    v3 v0 = s->v[3 * t], e1 = sub(s->v[3 * t + 1], v0), e2 = sub(s->v[3 * t + 2], v0);
+    float a[3] = {v0.x, v0.y, v0.z}, b[3] = {e1.x, e1.y, e1.z}, c[3] = {e2.x, e2.y, e2.z};
     for (int k = 0; k < 3; ++k) {
-        float p[3] = {s->v[3 * t + k].x, s->v[3 * t + k].y, s->v[3 * t + k].z};
-        for (int a = 0; a < 3; ++a) { if (p[a] < lo[a]) lo[a] = p[a]; if (p[a] > hi[a]) hi[a] = p[a]; }
+        float p1 = a[k] + b[k], p2 = a[k] + c[k];
+        float l = fminf(fminf(a[k], p1), p2), h = fmaxf(fmaxf(a[k], p1), p2);
+        lo[k] = l - box_pad(l);
+        hi[k] = h + box_pad(h);
     }
+}
+/* slab interval of a box; tn / tf without tmin / tmax */
+static inline void slab_interval(const float lo[3], const float hi[3], v3 inv, v3 io, float* tn, float* tf) {
+    float ax = fmaf(lo[0], inv.x, -io.x), bx = fmaf(hi[0], inv.x, -io.x);
+    float ay = fmaf(lo[1], inv.y, -io.y), by = fmaf(hi[1], inv.y, -io.y);
+    float az = fmaf(lo[2], inv.z, -io.z), bz = fmaf(hi[2], inv.z, -io.z);
+    *tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    *tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+}
+static int tri_accept(const orc_scene* s, int t, v3 inv, v3 io, float th) {
+    float lo[3], hi[3], tn, tf;
+    tri_bounds(s, t, lo, hi);
+    slab_interval(lo, hi, inv, io, &tn, &tf);
+    float tfk = tf * kSlabWiden;
+    return tn <= th * kSlabWiden && th <= tfk && tn <= tfk;
 }
 static float centroid(const orc_scene* s, int t, int a) {
     float lo[3], hi[3];
@@ -1005,12 +1038,6 @@ static int build_rec(orc_scene* s, int first, int count) {
             if (lo[a] < nd->lo[a]) nd->lo[a] = lo[a];
             if (hi[a] > nd->hi[a]) nd->hi[a] = hi[a];
         }
-    }
-    /* conservative padding so a slab test never culls a true hit */
-    for (int a = 0; a < 3; ++a) {
-        float ext = fmaxf(fabsf(nd->lo[a]), fabsf(nd->hi[a]));
-        float pad = ext * 1e-5f + 1e-6f;
-        nd->lo[a] -= pad; nd->hi[a] += pad;
     }
     if (count <= 4) { nd->left = nd->right = -1; nd->first = first; nd->count = count; return id; }
     int axis = 0;
@@ -1125,23 +1152,58 @@ static int tri_hit(const orc_scene* s, int t, v3 o, v3 d, float tmin, float tmax
     *th = tt; *uh = u; *vh = v; *back = det < 0.0f;
     return 1;
 }
-static int box_hit(const onode* nd, v3 o, v3 inv, float tmin, float tmax) {
-    float tn = tmin, tf = tmax;
-    float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
-    for (int a = 0; a < 3; ++a) {
-        float t0 = (nd->lo[a] - oo[a]) * ii[a];
-        float t1 = (nd->hi[a] - oo[a]) * ii[a];
-        if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
-        t1 *= 1.0000004f;
-        if (t0 > tn) tn = t0;   /* NaN (0*inf) comparisons are false: axis ignored */
-        if (t1 < tf) tf = t1;
-    }
-    return tn <= tf;
+static int box_hit(const onode* nd, v3 inv, v3 io, float tmin, float tmax) {
+    float tn, tf;
+    slab_interval(nd->lo, nd->hi, inv, io, &tn, &tf);
+    return fmaxf(tn, tmin) <= fminf(tf, tmax) * kSlabWiden;
+}
+static int trace_impl(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int anyhit, float* th,
+                      float* uh, float* vh, int* back, int cull);
+/* Cull check (diagnostic): every closest-hit trace is repeated without culling boxes by the
+ * current best t (only by [tmin, tmax]), i.e. the exhaustive (t, index) minimum over every
+ * triangle whose padded box the ray passes, and disagreements are counted. */
+static atomic_int g_cull_check;
+static atomic_ullong g_cull_traces, g_cull_mismatch;
+static float g_cull_first[16];
+static atomic_int g_cull_first_set;
+void orc_set_cull_check(int32_t on) {
+    atomic_store(&g_cull_check, on);
+    atomic_store(&g_cull_traces, 0);
+    atomic_store(&g_cull_mismatch, 0);
+    atomic_store(&g_cull_first_set, 0);
+}
+void orc_cull_check_stats(uint64_t out[2], float first[16]) {
+    out[0] = atomic_load(&g_cull_traces);
+    out[1] = atomic_load(&g_cull_mismatch);
+    memcpy(first, g_cull_first, sizeof g_cull_first);
 }
 static int trace(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int anyhit, float* th,
                  float* uh, float* vh, int* back) {
+    float t0 = 0, u0 = 0, v0 = 0;
+    int b0 = 0;
+    int r = trace_impl(s, o, d, tmin, tmax, anyhit, &t0, &u0, &v0, &b0, 1);
+    if (!anyhit && atomic_load_explicit(&g_cull_check, memory_order_relaxed)) {
+        float t1 = 0, u1 = 0, v1 = 0;
+        int b1 = 0;
+        int r1 = trace_impl(s, o, d, tmin, tmax, 0, &t1, &u1, &v1, &b1, 0);
+        atomic_fetch_add(&g_cull_traces, 1);
+        if (r1 != r || (r >= 0 && (t1 != t0 || u1 != u0 || v1 != v0))) {
+            atomic_fetch_add(&g_cull_mismatch, 1);
+            if (atomic_exchange(&g_cull_first_set, 1) == 0) {
+                float rec[16] = {o.x, o.y, o.z, d.x, d.y, d.z, tmin, tmax, (float)r, t0, (float)r1, t1,
+                                 u0, v0, u1, v1};
+                memcpy(g_cull_first, rec, sizeof rec);
+            }
+        }
+    }
+    if (r >= 0 && th) { *th = t0; *uh = u0; *vh = v0; *back = b0; }
+    return r;
+}
+static int trace_impl(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int anyhit, float* th,
+                      float* uh, float* vh, int* back, int cull) {
     if (s->ntri == 0) return -1;
-    v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    v3 inv = mk(ray_inv(d.x), ray_inv(d.y), ray_inv(d.z));
+    v3 io = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
     int stack[128];
     int sp = 0;
     stack[sp++] = 0;
@@ -1150,7 +1212,7 @@ static int trace(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int any
     int bb = 0;
     while (sp) {
         const onode* nd = &s->nodes[stack[--sp]];
-        if (!box_hit(nd, o, inv, tmin, bt)) continue;
+        if (!box_hit(nd, inv, io, tmin, cull ? bt : tmax)) continue;
         if (nd->left < 0) {
             for (int i = nd->first; i < nd->first + nd->count; ++i) {
                 int t = s->order[i];
@@ -1158,6 +1220,7 @@ static int trace(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int any
                 int bk;
                 if (!tri_hit(s, t, o, d, tmin, bt, &tt, &uu, &vv, &bk)) continue;
                 if (alpha_cut(s, t, uu, vv)) continue;  /* __anyhit__radiance/shadow */
+                if (!tri_accept(s, t, inv, io, tt)) continue;
                 if (anyhit) return t;
                 if (best < 0 || tt < bt || (tt == bt && t < best)) {
                     best = t; bt = tt; bu = uu; bv = vv; bb = bk;

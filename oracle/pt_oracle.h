@@ -104,6 +104,11 @@ int32_t orc_scene_triangles(const orc_scene* s);
 int32_t orc_trace_closest(const orc_scene* s, const float o[3], const float d[3], float tmin,
                           float tmax, float* t, float* u, float* v, int32_t* backface);
 int32_t orc_trace_any(const orc_scene* s, const float o[3], const float d[3], float tmin, float tmax);
+/* Diagnostic: repeat every closest-hit trace without culling by the running best t and count
+ * disagreements (out[0] traces, out[1] mismatches; first[16] = the first mismatching ray:
+ * o, d, tmin, tmax, prim, t, prim_exhaustive, t_exhaustive, u, v, u_exh, v_exh). */
+void orc_set_cull_check(int32_t on);
+void orc_cull_check_stats(uint64_t out[2], float first[16]);
 
 /* --- the hot path: per-pixel sum of radiance over frame ids [first_frame, first_frame+n_frames)
  *     for pixels x in [x0,x1), y in [y0,y1); sum_rgb is the full W*H*3 buffer (row 0 = bottom).

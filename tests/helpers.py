@@ -80,3 +80,47 @@ def random_rays(scene, n, seed=0, tmax=100.0):
     rays[:, 6] = 0.0
     rays[:, 7] = tmax
     return rays
+
+
+def shared_edge_rays(scene, n, seed=0, tmax=100.0, far=False):
+    """Rays aimed at points on edges shared by two triangles of a mesh, at grazing incidence
+    (cos in [1e-3, 0.08] to the first triangle's plane) from 0.5 to 90 units away -- or, with
+    far=True, from 40 to 95 units away in any direction.  These are the rays whose
+    Moller-Trumbore answer can lie outside the triangle's own box (the config-5 event of
+    round 1): both triangles of the edge may accept the hit with t a few ulps apart."""
+    rng = np.random.default_rng(seed)
+    pairs = []
+    for m in scene.meshes:
+        idx = np.asarray(m.indices)
+        edges = {}
+        for t, (a, b, c) in enumerate(idx):
+            for u, v in ((a, b), (b, c), (c, a)):
+                key = (min(u, v), max(u, v))
+                edges.setdefault(key, []).append(t)
+        shared = [(k, ts) for k, ts in edges.items() if len(ts) == 2]
+        if shared:
+            pairs.append((m, shared))
+    rays = np.zeros((n, 8), np.float32)
+    for i in range(n):
+        m, shared = pairs[rng.integers(len(pairs))]
+        (u, v), (ta, _) = shared[rng.integers(len(shared))]
+        V = np.asarray(m.vertices, np.float64)
+        s = rng.uniform(0.05, 0.95)
+        p = V[u] * (1 - s) + V[v] * s
+        tri = V[np.asarray(m.indices)[ta]]
+        nrm = np.cross(tri[1] - tri[0], tri[2] - tri[0])
+        nrm /= np.linalg.norm(nrm)
+        if far:
+            d = rng.normal(size=3)
+            dist = rng.uniform(40.0, 95.0)
+        else:
+            tng = np.cross(nrm, rng.normal(size=3))
+            tng /= np.linalg.norm(tng)
+            c = rng.uniform(1e-3, 0.08)
+            d = -np.sign(rng.uniform(-1, 1)) * c * nrm + np.sqrt(1 - c * c) * tng
+            dist = rng.uniform(0.5, 90.0)
+        d = d / np.linalg.norm(d)
+        rays[i, 0:3] = p - dist * d
+        rays[i, 3:6] = d
+        rays[i, 7] = tmax
+    return rays
