@@ -191,7 +191,10 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
             f"{p} not found: the HIP extension is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)"
         )
     lib = C.CDLL(str(p))
+    variant = path is None and "PTAMD_LIB" in os.environ
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue  # an older A/B build (tools/ab.sh) may predate an entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

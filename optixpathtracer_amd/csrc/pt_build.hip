@@ -53,8 +53,10 @@ __device__ __forceinline__ void tri_box(const float4* tri, int i, float lo[3], f
 }
 
 // The box the traversal's hit-acceptance rule uses for triangle i (pt_device.h tri_accept): the
-// vertices as the hit test sees them (v0, v0 + (v1 - v0), v0 + (v2 - v0)), padded.  All BVH
-// boxes are unions of these, so they contain every acceptance box bit for bit.
+// vertices as the hit test sees them (v0, v0 + (v1 - v0), v0 + (v2 - v0)), padded.  The boxes
+// stored in the BVH4 nodes are exact unions of these (k_sah_dp's refit), so they contain every
+// acceptance box bit for bit; the tree itself (PLOC clustering, SAH choices) is built on the
+// plain triangle boxes.
 __device__ __forceinline__ void tri_box_accept(const float4* tri, int i, float lo[3], float hi[3]) {
     const float4 a = tri[3 * i], b = tri[3 * i + 1], c = tri[3 * i + 2];
     const f3 v0 = mk(a.x, a.y, a.z);
@@ -79,7 +81,7 @@ __global__ void k_morton(const float4* tri, int n, float3 cmin, float3 cinv, uin
 // Leaf-order gather.  isect: v0|orig, (v1-v0)|material, (v2-v0)|alpha flag — the edge subtraction
 // is the same single fp32 op the oracle performs, so the hit arithmetic stays identical.
 __global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const float4* uv_orig, const uint32_t* order,
-                         int n, float4* isect, float4* shade, float4* tuv, float4* st0) {
+                         int n, float4* isect, float4* shade, float4* tuv, float4* st0, float4* pleaf) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     int i = (int)order[k];
@@ -97,9 +99,12 @@ __global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const f
     shade[4 * k + 2] = make_float4(na.z, nb.x, nb.y, nb.z);
     shade[4 * k + 3] = make_float4(nc.x, nc.y, nc.z, 0.0f);
     float lo[3], hi[3];
-    tri_box_accept(tri_orig, i, lo, hi);
+    tri_box(tri_orig, i, lo, hi);
     st0[2 * k] = make_float4(lo[0], lo[1], lo[2], 0.0f);
     st0[2 * k + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+    tri_box_accept(tri_orig, i, lo, hi);
+    pleaf[2 * k] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+    pleaf[2 * k + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
 }
 
 __global__ void k_sparse(const float4* prev, float4* cur, int count, int half) {
@@ -168,7 +173,19 @@ struct BinTree {
     const int2* range;
     const float4* box;  // internal node boxes (2 per node)
     const float4* leafbox;  // sparse table level 0 (2 per leaf)
+    const float4* pleaf;  // padded acceptance box per leaf (2 per leaf)
+    float4* pbox;         // union of the padded leaf boxes per internal node (k_sah_dp)
 };
+// Node box for the BVH4: the exact union of the padded acceptance boxes below `code`.
+__device__ __forceinline__ void code_box_padded(const BinTree& B, int code, float4& lo, float4& hi) {
+    if (code >= 0) {
+        lo = B.pbox[2 * code];
+        hi = B.pbox[2 * code + 1];
+    } else {
+        lo = B.pleaf[2 * ~code];
+        hi = B.pleaf[2 * ~code + 1];
+    }
+}
 
 __device__ __forceinline__ void code_box(const BinTree& B, int code, float4& lo, float4& hi) {
     if (code >= 0) {
@@ -246,19 +263,29 @@ __global__ void k_sah_dp(BinTree B, int n, const int* parent, const int* leafpar
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const int2 ch = B.child[node];
         float cl[5], cr[5];
+        float4 plo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), phi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
         const int kids[2] = {ch.x, ch.y};
         for (int k = 0; k < 2; ++k) {
             float* c = k == 0 ? cl : cr;
             const int code = kids[k];
+            float4 klo, khi;  // the child's padded box
             if (code < 0) {  // one triangle: always a leaf
                 float4 lo = B.leafbox[2 * ~code], hi = B.leafbox[2 * ~code + 1];
                 float v = half_area(lo, hi) * kSahCTri;
                 c[1] = c[2] = c[3] = c[4] = v;
+                klo = B.pleaf[2 * ~code];
+                khi = B.pleaf[2 * ~code + 1];
             } else {
                 float4 v = dp_load(dpc + code);
                 c[1] = v.x; c[2] = v.y; c[3] = v.z; c[4] = v.w;
+                klo = dp_load(B.pbox + 2 * code);
+                khi = dp_load(B.pbox + 2 * code + 1);
             }
+            plo = make_float4(fminf(plo.x, klo.x), fminf(plo.y, klo.y), fminf(plo.z, klo.z), 0.0f);
+            phi = make_float4(fmaxf(phi.x, khi.x), fmaxf(phi.y, khi.y), fmaxf(phi.z, khi.z), 0.0f);
         }
+        B.pbox[2 * node] = plo;
+        B.pbox[2 * node + 1] = phi;
         const float area = half_area(B.box[2 * node], B.box[2 * node + 1]);
         const int2 r = B.range[node];
         const int count = r.y - r.x + 1;
@@ -359,8 +386,8 @@ __global__ void k_collapse_emit(BinTree B, const int* dpd, const int* work, int 
             }
             continue;
         }
-        float4 l4, h4;  // already the union of padded acceptance boxes (tri_box_accept)
-        code_box(B, c[k], l4, h4);
+        float4 l4, h4;  // the exact union of the padded acceptance boxes below the child
+        code_box_padded(B, c[k], l4, h4);
         lo[0][k] = l4.x; lo[1][k] = l4.y; lo[2][k] = l4.z;
         hi[0][k] = h4.x; hi[1][k] = h4.y; hi[2][k] = h4.z;
         if (child_is_leaf(B, dpd, c[k])) {
@@ -401,7 +428,7 @@ __global__ void k_leafbox(const float4* tri_orig, const uint32_t* order, int n, 
     int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n) return;
     float lo[3], hi[3];
-    tri_box_accept(tri_orig, (int)order[m], lo, hi);
+    tri_box(tri_orig, (int)order[m], lo, hi);
     box[2 * m] = make_float4(lo[0], lo[1], lo[2], 0.0f);
     box[2 * m + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
     code[m] = ~m;
@@ -514,7 +541,7 @@ hipError_t ploc_build(const BuildInput& in, const uint32_t* morton_order, BuildO
         if (err == hipSuccess) owned.push_back(*p);
     };
     const int nb = n > 1 ? n - 1 : 1;
-    float4 *box[2] = {nullptr, nullptr}, *bbox = nullptr, *leafbox = nullptr;
+    float4 *box[2] = {nullptr, nullptr}, *bbox = nullptr, *leafbox = nullptr, *pleaf = nullptr;
     int *code[2] = {nullptr, nullptr}, *ccnt[2] = {nullptr, nullptr}, *nn = nullptr, *bcount = nullptr,
         *tot = nullptr;
     unsigned long long *flags = nullptr, *scan = nullptr;
@@ -536,6 +563,7 @@ hipError_t ploc_build(const BuildInput& in, const uint32_t* morton_order, BuildO
     alloc((void**)&bbox, sizeof(float4) * 2 * (size_t)nb);
     alloc((void**)&bcount, sizeof(int) * (size_t)nb);
     alloc((void**)&leafbox, sizeof(float4) * 2 * (size_t)n);
+    alloc((void**)&pleaf, sizeof(float4) * 2 * (size_t)n);
     alloc((void**)&dfs, sizeof(uint32_t) * (size_t)n);
     alloc((void**)&tot, sizeof(int) * 2);
     if (err != hipSuccess) return err;
@@ -593,12 +621,13 @@ hipError_t ploc_build(const BuildInput& in, const uint32_t* morton_order, BuildO
         }
     }
     hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig, in.uv_orig, dfs,
-                       n, out.isect, out.shade, out.tuv, leafbox);
+                       n, out.isect, out.shade, out.tuv, leafbox, pleaf);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     B.child = bchild;
     B.range = brange;
     B.box = bbox;
     B.leafbox = leafbox;
+    B.pleaf = pleaf;
     return hipSuccess;
 }
 
@@ -621,7 +650,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     int2 *bchild = nullptr, *brange = nullptr;
     int *work = nullptr, *work2 = nullptr, *wcnt = nullptr, *woff = nullptr;
     int *dp_parent = nullptr, *dp_leafparent = nullptr, *dp_visits = nullptr, *dp_dec = nullptr;
-    float4* dp_cost = nullptr;
+    float4 *dp_cost = nullptr, *lb_pleaf = nullptr, *pbox = nullptr;
     void* temp = nullptr;
     size_t temp_bytes = 0, scan_bytes = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -648,6 +677,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
         PT_TRY(hipMalloc(&bchild, sizeof(int2) * nbin));
         PT_TRY(hipMalloc(&brange, sizeof(int2) * nbin));
         PT_TRY(hipMalloc(&bbox, sizeof(float4) * 2 * nbin));
+        PT_TRY(hipMalloc(&lb_pleaf, sizeof(float4) * 2 * (size_t)n));
     }
     PT_TRY(hipMalloc(&work, sizeof(int) * n));
     PT_TRY(hipMalloc(&work2, sizeof(int) * n));
@@ -671,7 +701,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             PT_TRY(ploc_build(in, vals2, out, stream, B, root, owned));
         } else {
             hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig,
-                               in.uv_orig, vals2, n, out.isect, out.shade, out.tuv, st);
+                               in.uv_orig, vals2, n, out.isect, out.shade, out.tuv, st, lb_pleaf);
             PT_TRY(hipGetLastError());
             table.n = n;
             table.level[0] = st;
@@ -693,6 +723,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             B.range = brange;
             B.box = bbox;
             B.leafbox = st;
+            B.pleaf = lb_pleaf;
             root = n > 1 ? 0 : ~0;
         }
         if (root >= 0) {  // SAH DP over the binary tree (n >= 2)
@@ -701,6 +732,8 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             PT_TRY(hipMalloc(&dp_visits, sizeof(int) * nbin));
             PT_TRY(hipMalloc(&dp_cost, sizeof(float4) * nbin));
             PT_TRY(hipMalloc(&dp_dec, sizeof(int) * nbin));
+            PT_TRY(hipMalloc(&pbox, sizeof(float4) * 2 * nbin));
+            B.pbox = pbox;
             PT_TRY(hipMemsetAsync(dp_visits, 0, sizeof(int) * nbin, stream));
             PT_TRY(hipMemsetAsync(dp_parent, 0xff, sizeof(int) * nbin, stream));  // root: -1
             hipLaunchKernelGGL(k_parents, dim3(grid_for(nbin, 256)), dim3(256), 0, stream, B.child, nbin, dp_parent,
@@ -740,7 +773,8 @@ done:
     (void)hipStreamSynchronize(stream);
     for (void* p : {(void*)keys, (void*)vals, (void*)keys2, (void*)vals2, (void*)st, (void*)bchild, (void*)brange,
                     (void*)bbox, (void*)work, (void*)work2, (void*)wcnt, (void*)woff, temp, (void*)dp_parent,
-                    (void*)dp_leafparent, (void*)dp_visits, (void*)dp_cost, (void*)dp_dec})
+                    (void*)dp_leafparent, (void*)dp_visits, (void*)dp_cost, (void*)dp_dec, (void*)lb_pleaf,
+                    (void*)pbox})
         if (p) (void)hipFree(p);
     for (void* p : owned) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);

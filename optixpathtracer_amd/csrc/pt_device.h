@@ -215,7 +215,8 @@ struct TravState {
     int nx, ny, nz;    // byte offset (0 or 16) of the near slab plane per axis within the node
     bool any;          // any-hit ray (only read by kRayMixed traversals)
     bool strict;       // re-trace: only acceptable hits are taken (trav_restart_strict)
-    int path;          // wavefront extension rays: the path id, for the hit record
+    int path;          // closest-hit wavefront rays: the path id for the hit record; any-hit
+                       // rays: the bits of the hit's t once they stop (trav_result_ok)
     Hit h;
 };
 
@@ -389,6 +390,7 @@ __device__ __forceinline__ bool leaf_tri_eval(const DevScene& S, TravState& s, T
     if (is_any<ANY>(s)) {
         if (hit) {
             s.h.tri = ti;
+            s.path = __float_as_int(t);
             return true;
         }
     } else {
@@ -471,17 +473,19 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
 // A finished traversal's answer stands unless its hit is not acceptable (tri_accept) -- then
 // the ray is traced again in strict mode.  If the final hit is acceptable it IS the minimum
 // over the acceptable hits: every acceptable hit ordered before it had t <= best throughout,
-// so its boxes were never culled and it was tested and taken.  The check recomputes the hit
-// (same arithmetic, same t) from the triangle record; it runs once per finished ray.
-template <bool TEX>
+// so its boxes were never culled and it was tested and taken.  It runs once per finished ray,
+// on the hit's t kept by the traversal and the hit triangle's record (A, E1, E2).
+template <int ANY>
+__device__ __forceinline__ bool trav_hit_acceptable(const TravState& s, const float4 A, const float4 E1,
+                                                    const float4 E2) {
+    const float t = is_any<ANY>(s) ? __int_as_float(s.path) : s.h.t;
+    return tri_accept(A, E1, E2, s.inv, s.io, t);
+}
+template <int ANY, bool TEX>
 __device__ __forceinline__ bool trav_result_ok(const DevScene& S, const TravState& s) {
     if (s.strict || s.h.tri < 0) return true;
     const int ti = s.h.tri;
-    const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
-    float t, u, v;
-    bool bk;
-    (void)tri_test(A, E1, E2, s.o, s.d, s.tmin, s.best, t, u, v, bk);
-    return tri_accept(A, E1, E2, s.inv, s.io, t);
+    return trav_hit_acceptable<ANY>(s, S.isect[3 * ti], S.isect[3 * ti + 1], S.isect[3 * ti + 2]);
 }
 
 // Trace the ray again from the root, taking acceptable hits only.  Closest-hit lanes restart
@@ -513,7 +517,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tm
         while (true) {
             while (!trav_step<ANY, STATS, DEPTH, TEX>(S, s, stk, stride, spill, ts)) {
             }
-            if (trav_result_ok<TEX>(S, s)) break;
+            if (trav_result_ok<ANY, TEX>(S, s)) break;
             if (STATS) ts.retrace++;
             trav_restart_strict<ANY>(s, tmax);
         }

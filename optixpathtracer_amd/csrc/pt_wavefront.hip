@@ -213,7 +213,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         // at every step once the slice is drained
         if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
             if (done) {
-                if (trav_result_ok<TEX>(S, st)) {
+                if (trav_result_ok<ANY, TEX>(S, st)) {
                     finish(ri, st);
                     ri = -1;
                 } else {
