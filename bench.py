@@ -84,8 +84,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
                     help="PMC traffic per launch measured by tools/profile.sh (optional)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="override the config's scaling: strong = the step's spp in total, split over the "
+                         "ranks (for configs[1]: the one 1024-spp headline image rendered by N GPUs)")
     a = ap.parse_args()
-    scene, spp, a.scaling, a.workload = CONFIGS[a.config]
+    scene, spp, scaling, a.workload = CONFIGS[a.config]
+    a.scaling = a.scaling or scaling
     a.scene = a.scene or scene
     a.spp = a.spp or spp
     return a
@@ -170,6 +174,9 @@ def main():
         r.render_frames(first, n)
         r.synchronize()
         sharding.reduce_accumulator(accum, dist)  # RCCL over xGMI
+        # the reduce runs on torch's stream, the next step's clear and render on libptamd's:
+        # finish the reduce before this step ends, so the next clear cannot overtake it
+        torch.cuda.current_stream(dev).synchronize()
 
     for s in range(args.warmup):
         step(s)

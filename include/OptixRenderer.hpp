@@ -36,8 +36,10 @@ class OptixRendererT {
    public:
     ModelT* model;
 
+    // devices: empty = the single `device`; otherwise every listed device renders a share of
+    // the frame ids of RenderFrames / RenderAccumulate and RCCL sums the shares (pt_options.n_devices).
     OptixRendererT(const std::string& /*ptxPath*/, ModelT* m, int material_mode = PT_MAT_DEFAULT, int device = 0,
-                   int kernel = PT_KERNEL_AUTO)
+                   int kernel = PT_KERNEL_AUTO, const std::vector<int32_t>& devices = {})
         : model(m) {
         // Model::meshes (ModelLoading/Model.h:5-8) -> pt_mesh views (deep-copied by pt_create)
         std::vector<pt_mesh> meshes;
@@ -94,6 +96,8 @@ class OptixRendererT {
         opt.device = device;
         opt.material_mode = material_mode;
         opt.kernel = kernel;
+        opt.n_devices = (int32_t)devices.size();
+        opt.device_list = devices.empty() ? nullptr : devices.data();
         check(pt_create(&sc, &opt, &r_), "pt_create");
     }
     ~OptixRendererT() { pt_destroy(r_); }

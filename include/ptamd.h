@@ -84,7 +84,16 @@ typedef struct pt_options {
     int32_t material_mode;  /* PT_MAT_* */
     int32_t kernel;         /* PT_KERNEL_* */
     int32_t bvh_builder;    /* PT_BVH_* (replaces optixAccelBuild, OptixRenderer.cpp:306-456) */
-    int32_t reserved[4];
+    /* Multi-GPU inside the library (SURVEY.md §8(b) threading row, §8(e)).  0: one device
+     * (`device`), no RCCL.  n >= 1: the renderer drives n devices -- device_list[0..n), or
+     * device .. device+n-1 when device_list is NULL -- each with its own HIP stream, scene copy
+     * and BVH, plus one RCCL communicator over them created here.  pt_render_frames /
+     * pt_render_accumulate split their frame ids into n contiguous blocks (device g renders
+     * its block into its own fp32 sum) and ncclReduce the sums onto device_list[0], whose
+     * buffer pt_accum_* read.  pt_render / pt_launch / pt_display_* run on device_list[0]. */
+    int32_t n_devices;
+    int32_t reserved[3];
+    const int32_t* device_list;
 } pt_options;
 
 typedef struct pt_stats {
@@ -204,8 +213,13 @@ float* pt_accum_device_ptr(pt_renderer* r);
 /* Download the sum (scale = 1) or the mean (scale = 1/spp) to host. */
 int pt_accum_download(pt_renderer* r, float* host_rgb, float scale);
 
+/* Waits for every device of the renderer. */
 int pt_synchronize(pt_renderer* r);
-void* pt_stream(pt_renderer* r);   /* hipStream_t of the library */
+void* pt_stream(pt_renderer* r);   /* hipStream_t of the library (of device_list[0]) */
+/* Devices of a multi-device renderer (1 for a single-device one); ordinals into devices[]
+ * (at most max entries). */
+int32_t pt_device_count(const pt_renderer* r);
+int pt_devices(const pt_renderer* r, int32_t* devices, int32_t max);
 uint32_t pt_frame_id(const pt_renderer* r);
 int pt_set_frame_id(pt_renderer* r, uint32_t frame_id);
 int pt_get_stats(pt_renderer* r, pt_stats* out);

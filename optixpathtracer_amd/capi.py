@@ -71,7 +71,9 @@ class pt_options(C.Structure):
         ("material_mode", C.c_int32),
         ("kernel", C.c_int32),
         ("bvh_builder", C.c_int32),
-        ("reserved", C.c_int32 * 4),
+        ("n_devices", C.c_int32),
+        ("reserved", C.c_int32 * 3),
+        ("device_list", C.POINTER(C.c_int32)),
     ]
 
 
@@ -148,6 +150,8 @@ SIGNATURES = {
     "pt_accum_download": (C.c_int, [_R, _FP, C.c_float]),
     "pt_synchronize": (C.c_int, [_R]),
     "pt_stream": (C.c_void_p, [_R]),
+    "pt_device_count": (C.c_int32, [_R]),
+    "pt_devices": (C.c_int, [_R, C.POINTER(C.c_int32), C.c_int32]),
     "pt_frame_id": (C.c_uint32, [_R]),
     "pt_set_frame_id": (C.c_int, [_R, C.c_uint32]),
     "pt_get_stats": (C.c_int, [_R, C.POINTER(pt_stats)]),

@@ -5,6 +5,7 @@
 // There is no CPU fallback: every render and trace call runs the HIP kernels or fails
 // with a negative status.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -142,6 +143,11 @@ struct pt_renderer {
     uint64_t calls = 0;
     double bvh_ms = 0.0;
     int frames_per_launch = 64;  // 22 GB of queues at 1080p (16 -> 64 frames +5 % Lambert)
+    // multi-device (pt_options.n_devices >= 1): this renderer is device 0 of the list; peers are
+    // single-device renderers of the other devices; comms[g] is device g's RCCL communicator
+    std::vector<pt_renderer*> peers;
+    std::vector<ncclComm_t> comms;
+    float* d_part = nullptr;  // device 0's own partial sum (the total is accum())
 
     DevScene scene() const {
         DevScene S;
@@ -197,10 +203,11 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
     return L;
 }
 
-// Launch frames [first, first+n) in chunks, adding into accum; brackets with events.
+// Launch frames [first, first+n) in chunks, adding into accum; brackets with events.  Does not
+// wait for earlier work: the event pairs of every launch since the last synchronisation point
+// are summed at the next pt_synchronize / pt_get_stats / download (collect_pending).
 int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
-    int rc = collect_pending(r);
-    if (rc) return rc;
+    int rc = PT_OK;
     const DevScene S = r->scene();
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
@@ -268,6 +275,41 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
 
 bool valid_mode(int m) { return m >= PT_MAT_DEFAULT && m <= PT_MAT_LAYERED; }
 
+// Multi-device pt_render_frames: frame ids first .. first+n-1 split into contiguous blocks
+// (device g renders first + g*n/N .. , the same split as optixpathtracer_amd/sharding.py), each
+// device adding its block in frame order into its own fp32 sum; then one ncclReduce (sum) of
+// the N sums onto device 0's accum().  Every sample keeps its (pixel, frame id) seed, so the
+// image equals the single-device one up to the fp32 order of the N-way sum.  Each device's work
+// and its reduce are enqueued on that device's stream; nothing waits here.
+int render_frames_multi(pt_renderer* r, uint32_t first, uint32_t n) {
+    const int N = (int)r->comms.size();
+    const size_t count = 3 * (size_t)r->width * (size_t)r->height;
+    uint32_t f = first;
+    for (int g = 0; g < N; ++g) {
+        const uint32_t per = n / (uint32_t)N, extra = n % (uint32_t)N;
+        const uint32_t ng = per + ((uint32_t)g < extra ? 1u : 0u);
+        pt_renderer* d = g == 0 ? r : r->peers[(size_t)g - 1];
+        if (ng > 0) {
+            PT_HIP(hipSetDevice(d->device), "hipSetDevice");
+            const int rc = launch_frames(d, g == 0 ? r->d_part : d->accum(), f, ng);
+            if (rc) return rc;
+        }
+        f += ng;
+    }
+    ncclResult_t nr = ncclGroupStart();
+    for (int g = 0; g < N && nr == ncclSuccess; ++g) {
+        pt_renderer* d = g == 0 ? r : r->peers[(size_t)g - 1];
+        const float* send = g == 0 ? r->d_part : d->accum();
+        float* recv = g == 0 ? r->accum() : d->accum();  // significant on the root only
+        nr = ncclReduce(send, recv, count, ncclFloat32, ncclSum, 0, r->comms[(size_t)g], d->stream);
+    }
+    const ncclResult_t ne = ncclGroupEnd();
+    (void)hipSetDevice(r->device);
+    if (nr != ncclSuccess || ne != ncclSuccess)
+        return fail(PT_ERR_HIP, std::string("ncclReduce: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ne));
+    return PT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -282,6 +324,11 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         return fail(PT_ERR_INVALID, "pt_create: invalid scene");
     pt_options opt{};
     if (options) opt = *options;
+    // multi-device: validate the list, build device 0 here and the others as peers below
+    std::vector<int> devlist;
+    if (opt.n_devices < 0) return fail(PT_ERR_INVALID, "pt_create: negative n_devices");
+    for (int g = 0; g < opt.n_devices; ++g) devlist.push_back(opt.device_list ? opt.device_list[g] : opt.device + g);
+    if (!devlist.empty()) opt.device = devlist[0];
     if (!valid_mode(opt.material_mode)) return fail(PT_ERR_INVALID, "pt_create: invalid material_mode");
     if (opt.bvh_builder != PT_BVH_PLOC && opt.bvh_builder != PT_BVH_LBVH)
         return fail(PT_ERR_INVALID, "pt_create: invalid bvh_builder");
@@ -291,6 +338,11 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0) return fail(PT_ERR_HIP, "pt_create: no HIP device available");
     if (opt.device < 0 || opt.device >= ndev) return fail(PT_ERR_INVALID, "pt_create: device out of range");
+    for (size_t g = 0; g < devlist.size(); ++g) {
+        if (devlist[g] < 0 || devlist[g] >= ndev) return fail(PT_ERR_INVALID, "pt_create: device_list entry out of range");
+        for (size_t h = 0; h < g; ++h)
+            if (devlist[h] == devlist[g]) return fail(PT_ERR_INVALID, "pt_create: device_list repeats a device");
+    }
     PT_HIP(hipSetDevice(opt.device), "hipSetDevice");
 
     // ---- host: world-space triangle soup in original (mesh-concatenated) order ----
@@ -473,13 +525,47 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     }
     PT_HIPC(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
 #undef PT_HIPC
+    if (!devlist.empty()) {
+        // one single-device renderer per further device (own stream, scene copy, BVH build --
+        // the build is deterministic, so every device traces the same BVH), and one RCCL
+        // communicator over the list (ncclCommInitAll: a clique in this process)
+        for (size_t g = 1; g < devlist.size(); ++g) {
+            pt_options po = opt;
+            po.device = devlist[g];
+            po.n_devices = 0;
+            po.device_list = nullptr;
+            pt_renderer* p = nullptr;
+            int rc = pt_create(scene, &po, &p);
+            if (rc) {
+                const std::string msg = g_last_error;
+                pt_destroy(r);
+                return fail(rc, "pt_create (device " + std::to_string(devlist[g]) + "): " + msg);
+            }
+            r->peers.push_back(p);
+        }
+        r->comms.assign(devlist.size(), nullptr);
+        const ncclResult_t nr = ncclCommInitAll(r->comms.data(), (int)devlist.size(), devlist.data());
+        if (nr != ncclSuccess) {
+            r->comms.clear();
+            pt_destroy(r);
+            return fail(PT_ERR_HIP, std::string("pt_create: ncclCommInitAll: ") + ncclGetErrorString(nr));
+        }
+        (void)hipSetDevice(r->device);
+    }
     *out = r;
     return PT_OK;
 }
 
 int pt_destroy(pt_renderer* r) {
     if (!r) return PT_OK;
+    for (pt_renderer* p : r->peers) (void)hipSetDevice(p->device), (void)hipStreamSynchronize(p->stream);
+    (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
+    for (ncclComm_t c : r->comms)
+        if (c) (void)ncclCommDestroy(c);
+    for (pt_renderer* p : r->peers) pt_destroy(p);
+    (void)hipSetDevice(r->device);
+    if (r->d_part) (void)hipFree(r->d_part);
     (void)hipSetDevice(r->device);
     if (r->d_nodes) (void)hipFree(r->d_nodes);
     if (r->d_isect) (void)hipFree(r->d_isect);
@@ -505,21 +591,33 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
     if (!r) return fail(PT_ERR_INVALID, "pt_resize: NULL renderer");
     if (width < 0 || height < 0) return fail(PT_ERR_INVALID, "pt_resize: negative size");
     if (width == 0 || height == 0) return PT_OK;  // minimised window: no-op (OptixRenderer.cpp:651)
+    for (pt_renderer* p : r->peers) {
+        const int rc = pt_resize(p, width, height);
+        if (rc) return rc;
+    }
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     size_t bytes = sizeof(float) * 3 * (size_t)width * (size_t)height;
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_display) (void)hipFree(r->d_display);
-    r->d_frame = r->d_accum = r->d_display = nullptr;
+    if (r->d_part) (void)hipFree(r->d_part);
+    r->d_frame = r->d_accum = r->d_display = r->d_part = nullptr;
     r->display_ready = false;
+    // the size is committed only once every buffer exists (a failed allocation leaves an
+    // unsized renderer, on which the render calls return PT_ERR_STATE)
+    r->width = r->height = 0;
+    r->user_accum = nullptr;
     PT_HIP(hipMalloc(&r->d_frame, bytes), "hipMalloc frame");
     PT_HIP(hipMalloc(&r->d_accum, bytes), "hipMalloc accum");
     PT_HIP(hipMemsetAsync(r->d_accum, 0, bytes, r->stream), "hipMemset accum");
+    if (!r->comms.empty()) {
+        PT_HIP(hipMalloc(&r->d_part, bytes), "hipMalloc partial sum");
+        PT_HIP(hipMemsetAsync(r->d_part, 0, bytes, r->stream), "hipMemset partial sum");
+    }
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     r->width = width;
     r->height = height;
-    r->user_accum = nullptr;
     return PT_OK;
 }
 
@@ -529,16 +627,25 @@ int pt_set_camera(pt_renderer* r, const float position[3], const float inverse_v
     std::memcpy(r->cam_pos, position, sizeof r->cam_pos);
     std::memcpy(r->inv_view, inverse_view, sizeof r->inv_view);
     std::memcpy(r->inv_proj, inverse_projection, sizeof r->inv_proj);
+    for (pt_renderer* p : r->peers) (void)pt_set_camera(p, position, inverse_view, inverse_projection);
     return PT_OK;
 }
 
 int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count) {
     if (!r || count < 0 || (count > 0 && !lights)) return fail(PT_ERR_INVALID, "pt_set_lights: invalid");
+    for (pt_renderer* p : r->peers) {
+        const int rc = pt_set_lights(p, lights, count);
+        if (rc) return rc;
+    }
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     if (count > r->lights_cap) {
         PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
         if (r->d_lights) (void)hipFree(r->d_lights);
+        // no lights until the new array exists (a failed allocation must not leave a stale
+        // count over a NULL array)
         r->d_lights = nullptr;
+        r->n_lights = 0;
+        r->lights_cap = 0;
         PT_HIP(hipMalloc(&r->d_lights, sizeof(DevLight) * (size_t)count), "hipMalloc lights");
         r->lights_cap = count;
     }
@@ -562,12 +669,14 @@ int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces) {
     // enter SamplePath's loop, like 0, so it is rejected here rather than silently renamed
     if (max_bounces < 0) return fail(PT_ERR_INVALID, "pt_set_max_bounces: negative count");
     r->max_bounces = max_bounces;
+    for (pt_renderer* p : r->peers) p->max_bounces = max_bounces;
     return PT_OK;
 }
 
 int pt_set_material_mode(pt_renderer* r, int32_t mode) {
     if (!r || !valid_mode(mode)) return fail(PT_ERR_INVALID, "pt_set_material_mode: invalid");
     r->material_mode = mode;
+    for (pt_renderer* p : r->peers) p->material_mode = mode;
     return PT_OK;
 }
 
@@ -575,6 +684,7 @@ int pt_set_kernel(pt_renderer* r, int32_t kernel) {
     if (!r || (kernel != PT_KERNEL_MEGA && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_AUTO))
         return fail(PT_ERR_INVALID, "pt_set_kernel: invalid");
     r->kernel = kernel;
+    for (pt_renderer* p : r->peers) p->kernel = kernel;
     return PT_OK;
 }
 
@@ -676,9 +786,14 @@ int pt_display_download(pt_renderer* r, float* host_rgb) {
 int pt_accum_clear(pt_renderer* r) {
     if (!r) return fail(PT_ERR_INVALID, "pt_accum_clear: NULL");
     if (r->width == 0) return fail(PT_ERR_STATE, "pt_accum_clear: call pt_resize first");
+    for (pt_renderer* p : r->peers) {
+        const int rc = pt_accum_clear(p);
+        if (rc) return rc;
+    }
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
     PT_HIP(hipMemsetAsync(r->accum(), 0, bytes, r->stream), "hipMemset accum");
+    if (r->d_part) PT_HIP(hipMemsetAsync(r->d_part, 0, bytes, r->stream), "hipMemset partial sum");
     return PT_OK;
 }
 
@@ -687,7 +802,8 @@ int pt_render_frames(pt_renderer* r, uint32_t first_frame_id, uint32_t n_frames)
     if (r->width == 0) return fail(PT_ERR_STATE, "pt_render_frames: call pt_resize first");
     if (n_frames == 0) return PT_OK;
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
-    return launch_frames(r, r->accum(), first_frame_id, n_frames);
+    if (r->comms.empty()) return launch_frames(r, r->accum(), first_frame_id, n_frames);
+    return render_frames_multi(r, first_frame_id, n_frames);
 }
 
 int pt_render_accumulate(pt_renderer* r, uint32_t spp, uint32_t first_frame_id, float* host_rgb_mean) {
@@ -724,12 +840,22 @@ int pt_accum_download(pt_renderer* r, float* host_rgb, float scale) {
 
 int pt_synchronize(pt_renderer* r) {
     if (!r) return fail(PT_ERR_INVALID, "pt_synchronize: NULL");
+    for (pt_renderer* p : r->peers) {
+        const int rc = pt_synchronize(p);
+        if (rc) return rc;
+    }
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     return collect_pending(r);
 }
 
 void* pt_stream(pt_renderer* r) { return r ? (void*)r->stream : nullptr; }
+int32_t pt_device_count(const pt_renderer* r) { return r ? (int32_t)(1 + r->peers.size()) : 0; }
+int pt_devices(const pt_renderer* r, int32_t* devices, int32_t max) {
+    if (!r || max < 0 || (max > 0 && !devices)) return fail(PT_ERR_INVALID, "pt_devices: invalid");
+    for (int32_t g = 0; g < max && g < pt_device_count(r); ++g) devices[g] = g == 0 ? r->device : r->peers[g - 1]->device;
+    return PT_OK;
+}
 uint32_t pt_frame_id(const pt_renderer* r) { return r ? r->frame_id : 0u; }
 int pt_set_frame_id(pt_renderer* r, uint32_t frame_id) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_frame_id: NULL");
@@ -765,6 +891,22 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->trace_kernel_rays = c[6];
     out->trace_kernel_bytes = c[7];
     out->strict_retraces = c[8];
+    // a multi-device renderer reports the work of all its devices (times are device 0's)
+    for (pt_renderer* p : r->peers) {
+        pt_stats ps;
+        rc = pt_get_stats(p, &ps);
+        if (rc) return rc;
+        out->segments += ps.segments;
+        out->samples += ps.samples;
+        out->nodes_visited += ps.nodes_visited;
+        out->tri_tests += ps.tri_tests;
+        out->rays += ps.rays;
+        out->stack_overflows += ps.stack_overflows;
+        out->shadow_rays += ps.shadow_rays;
+        out->trace_kernel_rays += ps.trace_kernel_rays;
+        out->trace_kernel_bytes += ps.trace_kernel_bytes;
+        out->strict_retraces += ps.strict_retraces;
+    }
     return PT_OK;
 }
 
@@ -772,6 +914,10 @@ int pt_stats_reset(pt_renderer* r) {
     if (!r) return fail(PT_ERR_INVALID, "pt_stats_reset: NULL");
     int rc = pt_synchronize(r);
     if (rc) return rc;
+    for (pt_renderer* p : r->peers) {
+        if ((rc = pt_stats_reset(p)) != PT_OK) return rc;
+    }
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     PT_HIP(hipMemset(r->d_counters, 0, kCounters * sizeof(unsigned long long)), "hipMemset counters");
     r->samples = 0;
     r->last_ms = r->total_ms = 0.0;
@@ -785,6 +931,7 @@ int pt_stats_reset(pt_renderer* r) {
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames) {
     if (!r || frames < 1) return fail(PT_ERR_INVALID, "pt_set_frames_per_launch: invalid");
     r->frames_per_launch = frames;
+    for (pt_renderer* p : r->peers) p->frames_per_launch = frames;
     return PT_OK;
 }
 
@@ -916,6 +1063,7 @@ extern "C" int pt_bvh_download(pt_renderer* r, void* nodes, int64_t node_bytes, 
 extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_traversal_stats: NULL");
     r->trav_stats = enable != 0;
+    for (pt_renderer* p : r->peers) p->trav_stats = enable != 0;
     return PT_OK;
 }
 
@@ -924,6 +1072,9 @@ extern "C" int pt_set_primary_dedup(pt_renderer* r, int32_t enable) {
     int rc = collect_pending(r);
     if (rc) return rc;
     r->primary_dedup = enable != 0;
+    for (pt_renderer* p : r->peers) {
+        if ((rc = pt_set_primary_dedup(p, enable)) != PT_OK) return rc;
+    }
     return PT_OK;
 }
 
@@ -932,5 +1083,8 @@ extern "C" int pt_set_kernel_timing(pt_renderer* r, int32_t enable) {
     int rc = collect_pending(r);
     if (rc) return rc;
     r->kernel_timing = enable != 0;
+    for (pt_renderer* p : r->peers) {
+        if ((rc = pt_set_kernel_timing(p, enable)) != PT_OK) return rc;
+    }
     return PT_OK;
 }

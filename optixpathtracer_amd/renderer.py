@@ -85,7 +85,9 @@ class OptixRenderer:
     """Drop-in for `OptixRenderer` (OptixRenderer.h:8-110) backed by libptamd.so."""
 
     def __init__(self, ptx_path_or_none, model: Scene, device: int = 0, material_mode: int | None = None,
-                 kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC):
+                 kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC, devices=None):
+        """devices: None = the single `device`; a list of ordinals = one renderer over all of them
+        (frame ids of render_frames split across the devices, RCCL-summed onto devices[0])."""
         # ptxPath is accepted for signature compatibility and ignored (no PTX on gfx950).
         self.lib = load()
         self.model = model
@@ -95,6 +97,10 @@ class OptixRenderer:
         opts.material_mode = int(model.material_mode if material_mode is None else material_mode)
         opts.kernel = int(kernel)
         opts.bvh_builder = int(bvh_builder)
+        if devices is not None:
+            self._devlist = (C.c_int32 * max(1, len(devices)))(*[int(d) for d in devices])
+            opts.n_devices = len(devices)
+            opts.device_list = self._devlist
         h = C.c_void_p()
         check(self.lib.pt_create(C.byref(self._binding.scene), C.byref(opts), C.byref(h)), "pt_create")
         self.h = h
@@ -249,6 +255,13 @@ class OptixRenderer:
                                      1 if any_hit else 0), "pt_trace_rays")
         return prim, t, u, v, back
 
+    def devices(self) -> list:
+        """Device ordinals this renderer drives (pt_devices)."""
+        n = int(self.lib.pt_device_count(self.h))
+        out = (C.c_int32 * max(1, n))()
+        check(self.lib.pt_devices(self.h, out, n), "pt_devices")
+        return [int(out[i]) for i in range(n)]
+
     def bvh_arrays(self):
         """(nodes, triangles): the BVH4 node array as (bvh_nodes, 32) uint32 words and the
         leaf-ordered triangle records as (triangles, 12) uint32 words (pt_bvh_download)."""
@@ -272,9 +285,10 @@ class OptixRenderer:
 
 
 def setup_renderer(scene: Scene, width: int, height: int, max_bounces: int, device: int = 0,
-                   kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC) -> OptixRenderer:
+                   kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC,
+                   devices=None) -> OptixRenderer:
     """The reference's main.cpp:95-113 sequence: construct, Resize, SetLights, SetMaxBounces, SetCamera."""
-    r = OptixRenderer(None, scene, device=device, kernel=kernel, bvh_builder=bvh_builder)
+    r = OptixRenderer(None, scene, device=device, kernel=kernel, bvh_builder=bvh_builder, devices=devices)
     r.Resize((width, height))
     r.SetLights(scene.lights)
     r.SetMaxBounces(max_bounces)

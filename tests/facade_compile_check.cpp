@@ -6,6 +6,8 @@
 #include <memory>
 #include <vector>
 
+#include <cstring>
+
 #include "OptixRenderer.hpp"
 
 namespace stand_in {
@@ -88,7 +90,18 @@ int main() {
         float mm = 0.0f;
         for (const auto& v : mean) mm = v.x > mm ? v.x : mm;
         std::printf("accumulated max=%g\n", mm);
-        return (mx > 0.0f && mm > 0.0f) ? 0 : 3;
+        // multi-GPU inside the library: the same image from a renderer over a device list (one
+        // RCCL communicator; one device here, so the reduce must return the image bit for bit)
+        ptamd::OptixRendererT<Model> rm("ignored.ptx", &model, PT_MAT_LAMBERT, 0, PT_KERNEL_AUTO, {0});
+        rm.Resize(size);
+        rm.SetCamera(&cam);
+        rm.SetLights(&lights);
+        rm.SetMaxBounces(2);
+        std::vector<vec3> mean_multi(64);
+        rm.RenderAccumulate(4, 1, mean_multi.data());
+        const bool same = std::memcmp(mean.data(), mean_multi.data(), sizeof(vec3) * mean.size()) == 0;
+        std::printf("device-list image identical=%d\n", same ? 1 : 0);
+        return (mx > 0.0f && mm > 0.0f && same) ? 0 : 3;
     } catch (const std::exception& e) {
         std::printf("threw: %s\n", e.what());
         return 2;
