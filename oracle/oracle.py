@@ -94,6 +94,8 @@ def load() -> C.CDLL:
     lib.orc_bsdf_eval.argtypes = [C.c_int32, _UP, _FP, C.c_float, _FP, _FP, _FP]
     lib.orc_bsdf_pdf.restype = C.c_float
     lib.orc_bsdf_pdf.argtypes = [C.c_int32, C.c_float, _FP, _FP]
+    lib.orc_bsdf_sample_n.argtypes = [C.c_int32, _UP, _FP, C.c_float, _FP, C.c_int32, _FP, C.POINTER(C.c_int32)]
+    lib.orc_bsdf_pdf_n.argtypes = [C.c_int32, C.c_float, _FP, _FP, C.c_int32, _FP]
     lib.orc_cos_theta.restype = C.c_float
     lib.orc_cos_theta.argtypes = [_FP]
     lib.orc_furnace.argtypes = [C.c_int32, _UP, _FP, C.c_float, _FP, C.c_int32, _FP]
@@ -150,6 +152,24 @@ def bsdf_eval(model: str, seed: int, albedo, roughness: float, wo, wi):
     out = np.zeros(3, np.float32)
     load().orc_bsdf_eval(BSDF[model], C.byref(s), fp(_f(albedo)), float(roughness), fp(_f(wo)), fp(_f(wi)), fp(out))
     return out, int(s.value)
+
+
+def bsdf_sample_n(model: str, seed: int, albedo, roughness: float, wo, n: int):
+    """n samples of one wo with a running seed -> (ok[n] bool, out[n, 8], seed')."""
+    s = C.c_uint32(seed & 0xFFFFFFFF)
+    out = np.zeros((n, 8), np.float32)
+    ok = np.zeros(n, np.int32)
+    load().orc_bsdf_sample_n(BSDF[model], C.byref(s), fp(_f(albedo)), float(roughness), fp(_f(wo)), int(n), fp(out),
+                             ok.ctypes.data_as(C.POINTER(C.c_int32)))
+    return ok.astype(bool), out, int(s.value)
+
+
+def bsdf_pdf(model: str, roughness: float, wo, wi) -> np.ndarray:
+    """pdf of the model's Sample_f at directions wi (n, 3) for one wo."""
+    wi = _f(wi).reshape(-1, 3)
+    out = np.zeros(len(wi), np.float32)
+    load().orc_bsdf_pdf_n(BSDF[model], float(roughness), fp(_f(wo)), fp(wi), len(wi), fp(out))
+    return out
 
 
 def cos_theta(w) -> float:

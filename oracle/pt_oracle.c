@@ -787,11 +787,34 @@ void orc_furnace(int32_t model, uint32_t* seed, const float albedo[3], float rou
     out[0] = acc.x / (float)n; out[1] = acc.y / (float)n; out[2] = acc.z / (float)n;
 }
 
+/* Density of Conductor::Sample_f's direction (Conductor.h:123-189 computes it for the sampled
+ * wm: D(wo, wm) / (4 |wo.wm|)).  The reference has no Conductor::PDF; this is PBRT-v4's
+ * ConductorBxDF::PDF (wm = the half vector of wo and wi, faced to +z), used by the chi-square
+ * sampling test (tests/test_oracle_pins.py). */
+static float conductor_pdf(float roughness, v3 wo, v3 wi) {
+    float alpha = sqr(roughness);
+    if (!(wo.z * wi.z > 0.0f) || alpha < 1e-3f) return 0.0f;
+    v3 wm = add(wo, wi);
+    if (lensqr3(wm) == 0.0f) return 0.0f;
+    wm = normalize3(wm);
+    if (wm.z < 0.0f) wm = neg(wm);
+    return mf_pdf(wo, wm, alpha) / (4.0f * absdot(wo, wm));
+}
 float orc_bsdf_pdf(int32_t model, float roughness, const float wo[3], const float wi[3]) {
     v3 o = mk(wo[0], wo[1], wo[2]), i = mk(wi[0], wi[1], wi[2]);
     if (model == ORC_BSDF_LAMBERT) return lambert_pdf(o, i, 1);
     if (model == ORC_BSDF_DIELECTRIC) return dielectric_pdf(roughness, o, i, 1, 1);
+    if (model == ORC_BSDF_CONDUCTOR) return conductor_pdf(roughness, o, i);
     return 0.0f;
+}
+/* Batched forms for the statistical tests: n samples from one wo and a running seed; the pdf
+ * at n directions. */
+void orc_bsdf_sample_n(int32_t model, uint32_t* seed, const float albedo[3], float roughness, const float wo[3],
+                       int32_t n, float* out8, int32_t* ok) {
+    for (int32_t k = 0; k < n; ++k) ok[k] = orc_bsdf_sample(model, seed, albedo, roughness, wo, out8 + 8 * (size_t)k);
+}
+void orc_bsdf_pdf_n(int32_t model, float roughness, const float wo[3], const float* wi3, int32_t n, float* out) {
+    for (int32_t k = 0; k < n; ++k) out[k] = orc_bsdf_pdf(model, roughness, wo, wi3 + 3 * (size_t)k);
 }
 
 /* ------------------------------------------------------------------------------------ */

@@ -81,6 +81,9 @@ int32_t orc_bsdf_sample(int32_t model, uint32_t* seed, const float albedo[3], fl
 void orc_bsdf_eval(int32_t model, uint32_t* seed, const float albedo[3], float roughness,
                    const float wo[3], const float wi[3], float out[3]);
 float orc_bsdf_pdf(int32_t model, float roughness, const float wo[3], const float wi[3]);
+void orc_bsdf_sample_n(int32_t model, uint32_t* seed, const float albedo[3], float roughness, const float wo[3],
+                       int32_t n, float* out8, int32_t* ok);
+void orc_bsdf_pdf_n(int32_t model, float roughness, const float wo[3], const float* wi3, int32_t n, float* out);
 /* reference unit-test known answers (UnitTests/SpherGeom_Test.cpp) */
 float orc_cos_theta(const float w[3]);
 void orc_furnace(int32_t model, uint32_t* seed, const float albedo[3], float roughness, const float wo[3],
