@@ -33,6 +33,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -61,14 +62,42 @@ struct Json {
         const Json* v = get(key);
         return v && v->type == Num ? v->num : d;
     }
-    int int_or(const char* key, int d) const { return (int)num_or(key, (double)d); }
+    int int_or(const char* key, int d) const {  // d also for a non-finite or out-of-int-range number
+        const double x = num_or(key, (double)d);
+        return (std::isfinite(x) && x >= -2147483648.0 && x <= 2147483647.0) ? (int)x : d;
+    }
     std::string str_or(const char* key, const std::string& d) const {
         const Json* v = get(key);
         return v && v->type == Str ? v->str : d;
     }
     size_t size() const { return type == Arr ? arr.size() : 0; }
-    const Json& at(size_t i) const { return arr[i]; }
+    // bounds-checked: an index past the end (or into a non-array) reads as JSON null
+    const Json& at(size_t i) const {
+        static const Json null_value;
+        return (type == Arr && i < arr.size()) ? arr[i] : null_value;
+    }
 };
+
+// A JSON number used as an index or a size: finite, integral, in [0, limit).  Untrusted files
+// may hold negative, fractional, huge or non-numeric values; every conversion goes through here
+// (casting such a double to an integer is undefined behaviour).
+bool as_index(const Json* v, size_t limit, size_t& out) {
+    if (!v || v->type != Json::Num || !std::isfinite(v->num) || v->num < 0.0 || v->num != std::floor(v->num) ||
+        v->num >= (double)limit)
+        return false;
+    out = (size_t)v->num;
+    return true;
+}
+// An optional non-negative integer field (byteOffset, byteStride, count, ...); `d` when absent.
+bool size_field(const Json& o, const char* key, size_t d, size_t limit, size_t& out) {
+    const Json* v = o.get(key);
+    if (!v) {
+        out = d;
+        return true;
+    }
+    return as_index(v, limit, out);
+}
+constexpr size_t kMaxElements = (size_t)1 << 28;  // accessor counts, texels: refuse absurd sizes
 
 struct JsonParser {
     const char* p;
@@ -656,17 +685,20 @@ struct Loader {
             } else if (!read_file(base + uri_decode(uri), data)) {
                 return fail("gltf: cannot read buffer " + base + uri);
             }
-            if (data.size() < (size_t)b.num_or("byteLength", 0)) return fail("gltf: buffer shorter than byteLength");
+            size_t blen = 0;
+            if (!size_field(b, "byteLength", 0, (size_t)1 << 40, blen)) return fail("gltf: bad buffer byteLength");
+            if (data.size() < blen) return fail("gltf: buffer shorter than byteLength");
             buffers.push_back(std::move(data));
         }
         return true;
     }
 
     // Accessor -> floats (count * ncomp), with normalisation of integer types when asked.
-    bool read_accessor(int ai, int want_comp, std::vector<double>& vals, size_t& count) {
+    bool read_accessor(const Json* index, int want_comp, std::vector<double>& vals, size_t& count) {
         const Json* accs = root.get("accessors");
-        if (!accs || ai < 0 || (size_t)ai >= accs->size()) return fail("gltf: bad accessor index");
-        const Json& a = accs->at((size_t)ai);
+        size_t ai = 0;
+        if (!accs || !as_index(index, accs->size(), ai)) return fail("gltf: bad accessor index");
+        const Json& a = accs->at(ai);
         if (a.get("sparse")) return fail("gltf: sparse accessors are not supported");
         const std::string type = a.str_or("type", "");
         const int nc = type == "SCALAR" ? 1 : type == "VEC2" ? 2 : type == "VEC3" ? 3 : type == "VEC4" ? 4 : 0;
@@ -675,21 +707,27 @@ struct Loader {
         const int csize = (ct == 5120 || ct == 5121) ? 1 : (ct == 5122 || ct == 5123) ? 2 : (ct == 5125 || ct == 5126) ? 4 : 0;
         if (!csize) return fail("gltf: bad componentType");
         const bool norm = a.get("normalized") && a.get("normalized")->b;
-        count = (size_t)a.num_or("count", 0);
-        vals.assign(count * (size_t)nc, 0.0);
+        if (!size_field(a, "count", 0, kMaxElements, count)) return fail("gltf: bad accessor count");
         const Json* bvi = a.get("bufferView");
-        if (!bvi) return true;  // all zeros (glTF 2.0 §3.6.2.1)
+        if (!bvi) {  // all zeros (glTF 2.0 §3.6.2.1)
+            vals.assign(count * (size_t)nc, 0.0);
+            return true;
+        }
         const Json* views = root.get("bufferViews");
-        const int vi = (int)bvi->num;
-        if (!views || vi < 0 || (size_t)vi >= views->size()) return fail("gltf: bad bufferView index");
-        const Json& v = views->at((size_t)vi);
-        const int bi = v.int_or("buffer", -1);
-        if (bi < 0 || (size_t)bi >= buffers.size()) return fail("gltf: bad buffer index");
-        const std::vector<uint8_t>& buf = buffers[(size_t)bi];
-        const size_t off = (size_t)v.num_or("byteOffset", 0) + (size_t)a.num_or("byteOffset", 0);
+        size_t vi = 0, bi = 0, voff = 0, aoff = 0, stride = 0;
+        if (!views || !as_index(bvi, views->size(), vi)) return fail("gltf: bad bufferView index");
+        const Json& v = views->at(vi);
+        if (!as_index(v.get("buffer"), buffers.size(), bi)) return fail("gltf: bad buffer index");
+        const std::vector<uint8_t>& buf = buffers[bi];
         const size_t elem = (size_t)nc * (size_t)csize;
-        const size_t stride = v.get("byteStride") ? (size_t)v.num_or("byteStride", 0) : elem;
-        if (count && off + stride * (count - 1) + elem > buf.size()) return fail("gltf: accessor out of range");
+        if (!size_field(v, "byteOffset", 0, buf.size() + 1, voff) || !size_field(a, "byteOffset", 0, buf.size() + 1, aoff) ||
+            !size_field(v, "byteStride", elem, 256, stride) || stride < elem)
+            return fail("gltf: bad accessor offset or stride");
+        const size_t off = voff + aoff;
+        // overflow-free form of off + stride * (count - 1) + elem <= buf.size()
+        if (count && (off > buf.size() || elem > buf.size() - off || count - 1 > (buf.size() - off - elem) / stride))
+            return fail("gltf: accessor out of range");
+        vals.assign(count * (size_t)nc, 0.0);
         for (size_t i = 0; i < count; ++i) {
             const uint8_t* e = &buf[off + stride * i];
             for (int k = 0; k < nc; ++k) {
@@ -718,20 +756,21 @@ struct Loader {
         md.name = name;
         std::vector<double> vals;
         size_t nv = 0, cnt = 0;
-        if (!read_accessor((int)attrs->get("POSITION")->num, 3, vals, nv)) return false;
+        if (!read_accessor(attrs->get("POSITION"), 3, vals, nv)) return false;
+        if (nv > (size_t)0x7fffffff) return fail("gltf: too many vertices");
         md.v.assign(vals.begin(), vals.end());
         if (const Json* a = attrs->get("NORMAL")) {
-            if (!read_accessor((int)a->num, 3, vals, cnt)) return false;
+            if (!read_accessor(a, 3, vals, cnt)) return false;
             if (cnt != nv) return fail("gltf: NORMAL count differs from POSITION");
             md.n.assign(vals.begin(), vals.end());
         }
         if (const Json* a = attrs->get("TEXCOORD_0")) {
-            if (!read_accessor((int)a->num, 2, vals, cnt)) return false;
+            if (!read_accessor(a, 2, vals, cnt)) return false;
             if (cnt != nv) return fail("gltf: TEXCOORD_0 count differs from POSITION");
             md.uv.assign(vals.begin(), vals.end());
         }
         if (const Json* ii = prim.get("indices")) {
-            if (!read_accessor((int)ii->num, 1, vals, cnt)) return false;
+            if (!read_accessor(ii, 1, vals, cnt)) return false;
             for (double x : vals) {
                 if (x < 0 || x >= (double)nv) return fail("gltf: index out of range");
                 md.idx.push_back((int32_t)x);
@@ -766,23 +805,24 @@ struct Loader {
         return true;
     }
 
-    bool walk(int ni, const Mat4& parent, int depth) {
+    bool walk(const Json* index, const Mat4& parent, int depth) {
         const Json* nodes = root.get("nodes");
-        if (!nodes || ni < 0 || (size_t)ni >= nodes->size()) return fail("gltf: bad node index");
+        size_t ni = 0;
+        if (!nodes || !as_index(index, nodes->size(), ni)) return fail("gltf: bad node index");
         if (depth > 512) return fail("gltf: node hierarchy too deep (cycle?)");
-        const Json& node = nodes->at((size_t)ni);
+        const Json& node = nodes->at(ni);
         const Mat4 world = mul(parent, trs(node));
-        const int mi = node.int_or("mesh", -1);
-        if (mi >= 0) {
+        if (const Json* mj = node.get("mesh")) {
             const Json* meshes = root.get("meshes");
-            if (!meshes || (size_t)mi >= meshes->size()) return fail("gltf: bad mesh index");
-            const Json* prims = meshes->at((size_t)mi).get("primitives");
+            size_t mi = 0;
+            if (!meshes || !as_index(mj, meshes->size(), mi)) return fail("gltf: bad mesh index");
+            const Json* prims = meshes->at(mi).get("primitives");
             for (size_t p = 0; prims && p < prims->size(); ++p)
                 if (!add_primitive(prims->at(p), world, node.str_or("name", ""))) return false;
         }
         if (const Json* ch = node.get("children"))
             for (size_t k = 0; k < ch->size(); ++k)
-                if (!walk((int)ch->at(k).num, world, depth + 1)) return false;
+                if (!walk(&ch->at(k), world, depth + 1)) return false;
         return true;
     }
 
@@ -790,9 +830,9 @@ struct Loader {
         const Json* texs = root.get("textures");
         const Json* imgs = root.get("images");
         for (size_t i = 0; texs && i < texs->size(); ++i) {
-            const int src = texs->at(i).int_or("source", -1);
-            if (!imgs || src < 0 || (size_t)src >= imgs->size()) return fail("gltf: texture without image");
-            const Json& im = imgs->at((size_t)src);
+            size_t src = 0;
+            if (!imgs || !as_index(texs->at(i).get("source"), imgs->size(), src)) return fail("gltf: texture without image");
+            const Json& im = imgs->at(src);
             std::vector<uint8_t> bytes;
             const std::string uri = im.str_or("uri", "");
             if (!uri.empty()) {
@@ -803,10 +843,15 @@ struct Loader {
                     return fail("gltf: cannot read image " + base + uri);
                 }
             } else if (const Json* bv = im.get("bufferView")) {
-                const Json& v = root.get("bufferViews")->at((size_t)bv->num);
-                const std::vector<uint8_t>& b = buffers.at((size_t)v.int_or("buffer", 0));
-                const size_t off = (size_t)v.num_or("byteOffset", 0), len = (size_t)v.num_or("byteLength", 0);
-                if (off + len > b.size()) return fail("gltf: image bufferView out of range");
+                const Json* views = root.get("bufferViews");
+                size_t vi = 0, bi = 0, off = 0, len = 0;
+                if (!views || !as_index(bv, views->size(), vi)) return fail("gltf: bad image bufferView index");
+                const Json& v = views->at(vi);
+                if (!as_index(v.get("buffer"), buffers.size(), bi)) return fail("gltf: bad image buffer index");
+                const std::vector<uint8_t>& b = buffers[bi];
+                if (!size_field(v, "byteOffset", 0, b.size() + 1, off) || !size_field(v, "byteLength", 0, b.size() + 1, len) ||
+                    len > b.size() - off)
+                    return fail("gltf: image bufferView out of range");
                 bytes.assign(b.begin() + (long)off, b.begin() + (long)(off + len));
             }
             std::vector<uint32_t> px;
@@ -817,7 +862,8 @@ struct Loader {
             } else {
                 if (!decode) return fail("gltf: image " + std::to_string(src) + " is not PNG and no decoder was given");
                 int32_t dw = 0, dh = 0;
-                if (decode(bytes.data(), bytes.size(), &dw, &dh, nullptr, user) != 0 || dw <= 0 || dh <= 0)
+                if (decode(bytes.data(), bytes.size(), &dw, &dh, nullptr, user) != 0 || dw <= 0 || dh <= 0 ||
+                    (size_t)dw * (size_t)dh > kMaxElements)
                     return fail("gltf: decoder failed on image " + std::to_string(src));
                 px.assign((size_t)dw * (size_t)dh, 0);
                 if (decode(bytes.data(), bytes.size(), &dw, &dh, reinterpret_cast<uint8_t*>(px.data()), user) != 0)
@@ -838,7 +884,23 @@ extern "C" {
 
 const char* pt_model_last_error(void) { return g_gltf_error.c_str(); }
 
+static int load_gltf_impl(const char* path, pt_image_decode_fn decode, void* user, pt_model** out);
+
 int pt_model_load_gltf(const char* path, pt_image_decode_fn decode, void* user, pt_model** out) {
+    // nothing may unwind through the C ABI: an allocation failure (or any other exception)
+    // on a malformed file becomes an error status
+    try {
+        return load_gltf_impl(path, decode, user, out);
+    } catch (const std::exception& e) {
+        g_gltf_error = std::string("pt_model_load_gltf: ") + e.what();
+    } catch (...) {
+        g_gltf_error = "pt_model_load_gltf: unexpected exception";
+    }
+    if (out) *out = nullptr;
+    return PT_ERR_INVALID;
+}
+
+static int load_gltf_impl(const char* path, pt_image_decode_fn decode, void* user, pt_model** out) {
     if (!path || !out) {
         g_gltf_error = "pt_model_load_gltf: NULL argument";
         return PT_ERR_INVALID;
@@ -882,7 +944,7 @@ int pt_model_load_gltf(const char* path, pt_image_decode_fn decode, void* user, 
         if (scenes && si >= 0 && (size_t)si < scenes->size()) {
             const Json* nodes = scenes->at((size_t)si).get("nodes");
             for (size_t k = 0; ok && nodes && k < nodes->size(); ++k)
-                ok = L.walk((int)nodes->at(k).num, Mat4::identity(), 0);
+                ok = L.walk(&nodes->at(k), Mat4::identity(), 0);
         }
     }
     if (ok) ok = L.load_textures();

@@ -207,3 +207,62 @@ def test_scene_round_trip_through_gltf(tmp_path):
         np.testing.assert_array_equal(np.asarray(a.model, f).ravel(), b.model.ravel())
     for t0, t1 in zip(sc.textures, back.textures):
         np.testing.assert_array_equal(t0, t1)
+
+
+def _minimal(tmp_path, mutate):
+    """A one-triangle glTF with an embedded buffer, mutated by `mutate(doc)` before writing."""
+    v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32).tobytes()
+    i = np.array([0, 1, 2], np.uint32).tobytes()
+    buf = v + i
+    doc = {
+        "asset": {"version": "2.0"}, "scene": 0, "scenes": [{"nodes": [0]}],
+        "nodes": [{"mesh": 0, "children": []}],
+        "meshes": [{"primitives": [{"attributes": {"POSITION": 0}, "indices": 1}]}],
+        "buffers": [{"byteLength": len(buf),
+                     "uri": "data:application/octet-stream;base64," + base64.b64encode(buf).decode()}],
+        "bufferViews": [{"buffer": 0, "byteOffset": 0, "byteLength": 36},
+                        {"buffer": 0, "byteOffset": 36, "byteLength": 12}],
+        "accessors": [{"bufferView": 0, "componentType": 5126, "count": 3, "type": "VEC3"},
+                      {"bufferView": 1, "componentType": 5125, "count": 3, "type": "SCALAR"}],
+        "textures": [], "images": [],
+    }
+    mutate(doc)
+    p = tmp_path / "m.gltf"
+    p.write_text(json.dumps(doc))
+    return p
+
+
+MALFORMED = {
+    "huge-count": lambda d: d["accessors"][0].update(count=1e18),
+    "wrapping-count": lambda d: d["accessors"][0].update(count=2 ** 62),
+    "huge-stride": lambda d: d["bufferViews"][0].update(byteStride=2 ** 40),
+    "small-stride": lambda d: d["bufferViews"][0].update(byteStride=4),
+    "negative-offset": lambda d: d["accessors"][0].update(byteOffset=-8),
+    "fractional-accessor": lambda d: d["meshes"][0]["primitives"][0]["attributes"].update(POSITION=0.5),
+    "accessor-past-end": lambda d: d["meshes"][0]["primitives"][0]["attributes"].update(POSITION=7),
+    "bufferview-past-end": lambda d: d["accessors"][0].update(bufferView=9),
+    "buffer-past-end": lambda d: d["bufferViews"][0].update(buffer=3),
+    "string-node": lambda d: d["scenes"][0].update(nodes=["0"]),
+    "child-past-end": lambda d: d["nodes"][0].update(children=[5]),
+    "negative-mesh": lambda d: d["nodes"][0].update(mesh=-1e300),
+    "image-bufferview-past-end": lambda d: (d["textures"].append({"source": 0}),
+                                            d["images"].append({"bufferView": 40})),
+    "image-bad-buffer": lambda d: (d["textures"].append({"source": 0}), d["images"].append({"bufferView": 0}),
+                                   d["bufferViews"][0].update(buffer=-1)),
+    "texture-without-image": lambda d: d["textures"].append({"source": 2 ** 53}),
+    "nan-bytelength": lambda d: d["buffers"][0].update(byteLength=-1),
+}
+
+
+@pytest.mark.parametrize("name", sorted(MALFORMED))
+def test_load_gltf_rejects_malformed(tmp_path, name):
+    """ADVICE round 1 (pt_gltf.cpp:692,806): untrusted indices, counts, offsets and strides are
+    bounds-checked without overflow, so a malformed file is an error status, never a crash."""
+    p = _minimal(tmp_path, MALFORMED[name])
+    with pytest.raises(PTError):
+        gltf.load_gltf(p)
+
+
+def test_minimal_gltf_loads(tmp_path):
+    sc = gltf.load_gltf(_minimal(tmp_path, lambda d: None))
+    assert sc.n_triangles == 1
