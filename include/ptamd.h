@@ -237,6 +237,25 @@ int pt_camera_from_blender(const float blender_position[3], const float blender_
 int pt_trace_rays(pt_renderer* r, const float* host_rays, int32_t n, int32_t* prim, float* t,
                   float* u, float* v, int32_t* backface, int32_t any_hit);
 
+/* Debug path: the reference's isDebugRay (devicePrograms.cu:637-644, printed at :428-437) as
+ * data.  While set, the path of pixel (x, y) (row 0 = bottom) at frame frame_id records every
+ * bounce it shades -- in whichever render call covers that frame, on device_list[0] -- and
+ * pt_get_debug_path downloads the records (at most max; *n_bounces = how many were recorded).
+ * x < 0 turns it off.  The CPU oracle records the same fields (oracle orc_sample_path_debug). */
+typedef struct pt_debug_bounce {
+    int32_t bounce;             /* rayData->bounceCounter after the hit (devicePrograms.cu:360), 1.. */
+    int32_t prim;               /* global triangle index of the hit */
+    float position[3];          /* surface.position */
+    float albedo[3];            /* surface.albedo (after SampleTextures) */
+    float shading_normal[3];    /* surface.sNormal (face-forwarded, back-face flipped, normal-mapped) */
+    float geometry_normal[3];   /* surface.gNormal */
+    float roughness, metallic;
+    float beta[3];              /* path throughput entering the bounce */
+    float radiance[3];          /* path radiance gathered before the bounce's NEE */
+} pt_debug_bounce;
+int pt_set_debug_pixel(pt_renderer* r, int32_t x, int32_t y, uint32_t frame_id);
+int pt_get_debug_path(pt_renderer* r, pt_debug_bounce* out, int32_t max, int32_t* n_bounces);
+
 /* Debug / determinism: copy the BVH4 node array (128 B per node, pt_stats.bvh_nodes nodes) and
  * the leaf-ordered triangle records (48 B per triangle) to host; at most the given byte counts. */
 int pt_bvh_download(pt_renderer* r, void* nodes, int64_t node_bytes, void* triangles, int64_t triangle_bytes);

@@ -77,6 +77,21 @@ class pt_options(C.Structure):
     ]
 
 
+class pt_debug_bounce(C.Structure):
+    _fields_ = [
+        ("bounce", C.c_int32),
+        ("prim", C.c_int32),
+        ("position", C.c_float * 3),
+        ("albedo", C.c_float * 3),
+        ("shading_normal", C.c_float * 3),
+        ("geometry_normal", C.c_float * 3),
+        ("roughness", C.c_float),
+        ("metallic", C.c_float),
+        ("beta", C.c_float * 3),
+        ("radiance", C.c_float * 3),
+    ]
+
+
 class pt_stats(C.Structure):
     _fields_ = [
         ("segments", C.c_uint64),
@@ -159,6 +174,8 @@ SIGNATURES = {
     "pt_camera_from_blender": (C.c_int, [_FP, _FP, C.c_float, C.c_int32, C.c_int32, _FP, _FP, _FP]),
     "pt_trace_rays": (C.c_int, [_R, _FP, C.c_int32, _IP, _FP, _FP, _FP, _IP, C.c_int32]),
     "pt_bvh_download": (C.c_int, [_R, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]),
+    "pt_set_debug_pixel": (C.c_int, [_R, C.c_int32, C.c_int32, C.c_uint32]),
+    "pt_get_debug_path": (C.c_int, [_R, C.POINTER(pt_debug_bounce), C.c_int32, C.POINTER(C.c_int32)]),
     "pt_last_error": (C.c_char_p, []),
     "pt_version": (C.c_char_p, []),
     "pt_display_reset": (C.c_int, [_R, C.c_int32]),

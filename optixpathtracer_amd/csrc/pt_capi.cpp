@@ -148,6 +148,10 @@ struct pt_renderer {
     std::vector<pt_renderer*> peers;
     std::vector<ncclComm_t> comms;
     float* d_part = nullptr;  // device 0's own partial sum (the total is accum())
+    // debug path (pt_set_debug_pixel): pixel W*y+x (-1 = off), frame id, per-bounce records
+    int debug_pixel = -1;
+    uint32_t debug_frame = 0;
+    float* d_debug = nullptr;
 
     DevScene scene() const {
         DevScene S;
@@ -200,6 +204,9 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
     L.n_frames = n_frames;
     L.accum = accum;
     L.counters = r->d_counters;
+    L.debug_pixel = r->d_debug ? r->debug_pixel : -1;
+    L.debug_frame = r->debug_frame;
+    L.debug = r->d_debug;
     return L;
 }
 
@@ -579,6 +586,7 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_display) (void)hipFree(r->d_display);
     if (r->d_counters) (void)hipFree(r->d_counters);
+    if (r->d_debug) (void)hipFree(r->d_debug);
     wavefront_free(r->wf);
     r->ev.destroy();
     r->tev.destroy();
@@ -1057,6 +1065,41 @@ extern "C" int pt_bvh_download(pt_renderer* r, void* nodes, int64_t node_bytes, 
     const int64_t tb = std::min<int64_t>(triangle_bytes, (int64_t)sizeof(float4) * 3 * r->ntri);
     if (nb > 0) PT_HIP(hipMemcpy(nodes, r->d_nodes, (size_t)nb, hipMemcpyDeviceToHost), "download nodes");
     if (tb > 0) PT_HIP(hipMemcpy(triangles, r->d_isect, (size_t)tb, hipMemcpyDeviceToHost), "download triangles");
+    return PT_OK;
+}
+
+extern "C" int pt_set_debug_pixel(pt_renderer* r, int32_t x, int32_t y, uint32_t frame_id) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_debug_pixel: NULL");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    if (x < 0 || y < 0) {  // off
+        r->debug_pixel = -1;
+        return PT_OK;
+    }
+    if (r->width == 0 || x >= r->width || y >= r->height)
+        return fail(PT_ERR_INVALID, "pt_set_debug_pixel: pixel outside the frame (call pt_resize first)");
+    const size_t bytes = sizeof(float) * kDebugRecordFloats * kDebugMaxBounces;
+    if (!r->d_debug) PT_HIP(hipMalloc(&r->d_debug, bytes), "hipMalloc debug records");
+    PT_HIP(hipMemset(r->d_debug, 0, bytes), "hipMemset debug records");
+    r->debug_pixel = r->width * y + x;
+    r->debug_frame = frame_id;
+    return PT_OK;
+}
+
+extern "C" int pt_get_debug_path(pt_renderer* r, pt_debug_bounce* out, int32_t max, int32_t* n_bounces) {
+    static_assert(sizeof(pt_debug_bounce) == sizeof(float) * kDebugRecordFloats, "pt_debug_bounce layout");
+    if (!r || max < 0 || (max > 0 && !out) || !n_bounces) return fail(PT_ERR_INVALID, "pt_get_debug_path: invalid");
+    *n_bounces = 0;
+    if (!r->d_debug) return fail(PT_ERR_STATE, "pt_get_debug_path: call pt_set_debug_pixel first");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    std::vector<pt_debug_bounce> rec(kDebugMaxBounces);
+    PT_HIP(hipMemcpy(rec.data(), r->d_debug, sizeof(pt_debug_bounce) * rec.size(), hipMemcpyDeviceToHost),
+           "download debug records");
+    int n = 0;
+    while (n < kDebugMaxBounces && rec[(size_t)n].bounce == n + 1) ++n;
+    *n_bounces = n;
+    for (int k = 0; k < n && k < max; ++k) out[k] = rec[(size_t)k];
     return PT_OK;
 }
 

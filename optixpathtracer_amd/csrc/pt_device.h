@@ -61,7 +61,21 @@ struct DevLaunch {
     uint32_t n_frames;
     float* accum;                    // W*H*3 fp32 sum
     unsigned long long* counters;    // [0] segments [1] nodes visited [2] triangle tests [3] rays
+    // debug path (pt_set_debug_pixel; the reference's isDebugRay, devicePrograms.cu:637-644):
+    // the path of pixel debug_pixel (W*y + x, -1 = off) at frame debug_frame records every
+    // bounce's surface into debug[bounce - 1] (kDebugRecordFloats floats each)
+    int debug_pixel;
+    uint32_t debug_frame;
+    float* debug;
 };
+constexpr int kDebugMaxBounces = 64;
+constexpr int kDebugRecordFloats = 22;  // ptamd.h pt_debug_bounce
+
+// Wavefront path id of the debug path in the batch of L (path = frame offset * pixels + pixel), or -1.
+__device__ __forceinline__ int debug_path_id(const DevLaunch& L) {
+    const uint32_t f = L.debug_frame - L.frame_base;
+    return (L.debug_pixel >= 0 && f < L.n_frames) ? (int)f * L.width * L.height + L.debug_pixel : -1;
+}
 
 struct Hit {
     float t, u, v;
@@ -647,6 +661,22 @@ __device__ __forceinline__ void path_start(PathState& p, f3 o, f3 d, uint32_t se
     p.end = false;
 }
 
+// The reference's debug print of one bounce of the debug path (devicePrograms.cu:428-437:
+// position, albedo, shading and geometry normal, roughness, metallic, at bounceCounter), plus
+// the hit triangle's global index, the throughput entering the bounce and the radiance so far.
+// Record layout: ptamd.h pt_debug_bounce.
+__device__ __forceinline__ void debug_record(const DevLaunch& L, int bounce, int prim, const SurfaceHit& sf, f3 beta,
+                                             f3 radiance) {
+    if (bounce < 1 || bounce > kDebugMaxBounces) return;
+    float* r = L.debug + (size_t)(bounce - 1) * kDebugRecordFloats;
+    const float v[kDebugRecordFloats] = {__int_as_float(bounce), __int_as_float(prim),
+                                         sf.pos.x, sf.pos.y, sf.pos.z, sf.albedo.x, sf.albedo.y, sf.albedo.z,
+                                         sf.fr.n.x, sf.fr.n.y, sf.fr.n.z, sf.ng.x, sf.ng.y, sf.ng.z,
+                                         sf.roughness, sf.metallic, beta.x, beta.y, beta.z,
+                                         radiance.x, radiance.y, radiance.z};
+    for (int k = 0; k < kDebugRecordFloats; ++k) r[k] = v[k];
+}
+
 // loop test of SamplePath (devicePrograms.cu:646)
 __device__ __forceinline__ bool path_alive(const DevLaunch& L, const PathState& p) {
     return !p.end && p.bounce < L.max_bounces && length(p.beta) > 0.00001f;
@@ -656,7 +686,7 @@ __device__ __forceinline__ bool path_alive(const DevLaunch& L, const PathState& 
 // (devicePrograms.cu:343-514) or __miss__radiance (:576-583).  Returns false on a miss.
 template <int MODE, bool STATS, int DEPTH, bool TEX>
 __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch& L, PathState& p, int* stk,
-                                             int stride, TravStats& ts) {
+                                             int stride, TravStats& ts, bool debug_path) {
     Hit h;
     bool hit = traverse<false, STATS, DEPTH, TEX>(S, p.o, p.d, 0.0f, 100.0f, h, stk, stride, ts);
     if (!hit) {
@@ -671,6 +701,7 @@ __device__ __forceinline__ void path_segment(const DevScene& S, const DevLaunch&
     }
     SurfaceHit sf;
     reconstruct<TEX>(S, h, p.d, sf);
+    if (debug_path) debug_record(L, p.bounce, __float_as_int(S.isect[3 * h.tri].w), sf, p.beta, p.radiance);
     const bool conductor = rnd(p.seed) < sf.metallic;  // :400
     // NEE (:446-472), Lighting::GetRandomPointLight (LightMethods.h:25-40)
     float P = 0.0f;

@@ -73,9 +73,11 @@ __global__ __launch_bounds__(kBlock, PT_MK_WAVES) void k_render_mega(DevScene S,
         uint32_t f = 0;
         PathState p;
         path_start(p, co, cd, tea16(pix, L.frame_base));  // devicePrograms.cu:631
+        const bool debug_pixel = L.debug_pixel == (int)pix;
         while (true) {
             if (path_alive(L, p)) {
-                path_segment<MODE, STATS, kStack, TEX>(S, L, p, stk, kBlock, ts);
+                path_segment<MODE, STATS, kStack, TEX>(S, L, p, stk, kBlock, ts,
+                                                       debug_pixel && L.frame_base + f == L.debug_frame);
                 segs++;
                 continue;
             }

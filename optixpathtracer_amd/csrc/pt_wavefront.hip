@@ -388,6 +388,10 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 float4 bv = ldqs(W.beta + path);
                 uint32_t seed = __float_as_uint(bv.w);
                 f3 beta = mk(bv.x, bv.y, bv.z);
+                if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
+                    const float4 l = W.L[path];
+                    debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, beta, mk(l.x, l.y, l.z));
+                }
                 const bool conductor = rnd(seed) < sf.metallic;  // :400
                 int li;
                 const float P = pick_light(L, seed, li);
@@ -522,6 +526,11 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
                 reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
                 float4 bv = W.beta[path];
                 uint32_t seed = __float_as_uint(bv.w);
+                if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
+                    const float4 l = W.L[path];
+                    debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, mk(bv.x, bv.y, bv.z),
+                                 mk(l.x, l.y, l.z));
+                }
                 const bool conductor = rnd(seed) < sf.metallic;
                 int li;
                 const float P = pick_light(L, seed, li);

@@ -255,6 +255,23 @@ class OptixRenderer:
                                      1 if any_hit else 0), "pt_trace_rays")
         return prim, t, u, v, back
 
+    def set_debug_pixel(self, x: int, y: int, frame_id: int) -> None:
+        """Record the per-bounce surface of pixel (x, y)'s path at frame_id (pt_set_debug_pixel;
+        the reference's isDebugRay, devicePrograms.cu:637-644).  x < 0 turns it off."""
+        check(self.lib.pt_set_debug_pixel(self.h, int(x), int(y), int(frame_id)), "pt_set_debug_pixel")
+
+    def debug_path(self) -> list:
+        """The recorded bounces as dicts of pt_debug_bounce fields."""
+        recs = (capi.pt_debug_bounce * 64)()
+        n = C.c_int32()
+        check(self.lib.pt_get_debug_path(self.h, recs, 64, C.byref(n)), "pt_get_debug_path")
+        out = []
+        for k in range(n.value):
+            r = recs[k]
+            out.append({f: (list(getattr(r, f)) if isinstance(getattr(r, f), C.Array) else getattr(r, f))
+                        for f, _ in capi.pt_debug_bounce._fields_})
+        return out
+
     def devices(self) -> list:
         """Device ordinals this renderer drives (pt_devices)."""
         n = int(self.lib.pt_device_count(self.h))

@@ -117,6 +117,9 @@ def load() -> C.CDLL:
                                C.c_int32, C.c_int32, _FP, C.c_int32, C.POINTER(C.c_uint64)]
     lib.orc_sample_path.argtypes = [C.c_void_p, C.POINTER(orc_launch), C.c_int32, C.c_int32, C.c_uint32, _FP,
                                     C.POINTER(C.c_int32)]
+    lib.orc_sample_path_debug.restype = C.c_int32
+    lib.orc_sample_path_debug.argtypes = [C.c_void_p, C.POINTER(orc_launch), C.c_int32, C.c_int32, C.c_uint32, _FP,
+                                          C.c_int32, _FP]
     _lib = lib
     return lib
 
@@ -275,6 +278,15 @@ class OracleScene:
         segs = C.c_int32()
         self.lib.orc_sample_path(self.h, C.byref(lp), x, y, frame, fp(out), C.byref(segs))
         return out, int(segs.value)
+
+    def sample_path_debug(self, lp, x, y, frame, max_bounces=64):
+        """The debug pixel's per-bounce records (orc_sample_path_debug; ptamd.h pt_debug_bounce
+        layout) as a (bounces, 22) float32 array (bounce and prim are int32 bits) and the path's
+        radiance."""
+        rec = np.zeros((max_bounces, 22), np.float32)
+        rgb = np.zeros(3, np.float32)
+        n = self.lib.orc_sample_path_debug(self.h, C.byref(lp), x, y, frame, fp(rec), max_bounces, fp(rgb))
+        return rec[:n], rgb
 
     def trace(self, rays, any_hit=False):
         r = _f(rays).reshape(-1, 8)

@@ -1272,7 +1272,7 @@ int32_t orc_trace_any(const orc_scene* s, const float o[3], const float d[3], fl
 /* The path — SamplePath (devicePrograms.cu:625-664) + __closesthit__radiance (:343-514)  */
 /* ------------------------------------------------------------------------------------ */
 static v3 sample_path(const orc_scene* s, const orc_launch* lp, v3 origin, v3 dir, uint32_t seed,
-                      int* segs) {
+                      int* segs, float* dbg, int dbg_max) {
     v3 radiance = mk(0, 0, 0), beta = mk(1, 1, 1);
     int bounce = 0, endPath = 0;
     v3 o = origin, d = dir;
@@ -1350,6 +1350,19 @@ static v3 sample_path(const orc_scene* s, const orc_launch* lp, v3 origin, v3 di
                        (T0.z * tn.x + B0.z * tn.y) + Ns.z * tn.z);
             Ns = normalize3(wn);
         }
+        if (dbg && bounce <= dbg_max) {  /* debug print of devicePrograms.cu:428-437, as data */
+            float* r = dbg + (size_t)(bounce - 1) * ORC_DEBUG_FLOATS;
+            int32_t ib = bounce, ip = prim;
+            memcpy(&r[0], &ib, 4);
+            memcpy(&r[1], &ip, 4);
+            r[2] = pos.x; r[3] = pos.y; r[4] = pos.z;
+            r[5] = sf.albedo.x; r[6] = sf.albedo.y; r[7] = sf.albedo.z;
+            r[8] = Ns.x; r[9] = Ns.y; r[10] = Ns.z;
+            r[11] = Ng.x; r[12] = Ng.y; r[13] = Ng.z;
+            r[14] = sf.roughness; r[15] = metallic;
+            r[16] = beta.x; r[17] = beta.y; r[18] = beta.z;
+            r[19] = radiance.x; r[20] = radiance.y; r[21] = radiance.z;
+        }
         /* GetTBN / BuildTangentSpace :168-212 */
         v3 c1 = cross3(Ns, mk(0.0f, 0.0f, 1.0f));
         v3 c2 = cross3(Ns, mk(0.0f, 1.0f, 0.0f));
@@ -1413,9 +1426,27 @@ void orc_sample_path(const orc_scene* s, const orc_launch* lp, int32_t x, int32_
     orc_camera_ray(lp, x, y, o, d);
     uint32_t seed = orc_tea16((uint32_t)(lp->width * y + x), frame);  /* :631 */
     int segs = 0;
-    v3 r = sample_path(s, lp, mk(o[0], o[1], o[2]), mk(d[0], d[1], d[2]), seed, &segs);
+    v3 r = sample_path(s, lp, mk(o[0], o[1], o[2]), mk(d[0], d[1], d[2]), seed, &segs, NULL, 0);
     out_rgb[0] = r.x; out_rgb[1] = r.y; out_rgb[2] = r.z;
     if (segments) *segments = segs;
+}
+int32_t orc_sample_path_debug(const orc_scene* s, const orc_launch* lp, int32_t x, int32_t y, uint32_t frame,
+                              float* records, int32_t max_bounces, float out_rgb[3]) {
+    float o[3], d[3];
+    orc_camera_ray(lp, x, y, o, d);
+    uint32_t seed = orc_tea16((uint32_t)(lp->width * y + x), frame);
+    int segs = 0;
+    memset(records, 0, sizeof(float) * ORC_DEBUG_FLOATS * (size_t)(max_bounces > 0 ? max_bounces : 0));
+    v3 r = sample_path(s, lp, mk(o[0], o[1], o[2]), mk(d[0], d[1], d[2]), seed, &segs, records, max_bounces);
+    out_rgb[0] = r.x; out_rgb[1] = r.y; out_rgb[2] = r.z;
+    int n = 0;
+    while (n < max_bounces) {
+        int32_t b;
+        memcpy(&b, &records[(size_t)n * ORC_DEBUG_FLOATS], 4);
+        if (b != n + 1) break;
+        ++n;
+    }
+    return n;
 }
 
 typedef struct {
@@ -1442,7 +1473,7 @@ static void* worker(void* arg) {
             for (uint32_t f = 0; f < J->nf; ++f) {
                 uint32_t seed = orc_tea16((uint32_t)(J->lp->width * y + x), J->f0 + f);
                 int segs = 0;
-                v3 r = sample_path(J->s, J->lp, mk(o[0], o[1], o[2]), mk(d[0], d[1], d[2]), seed, &segs);
+                v3 r = sample_path(J->s, J->lp, mk(o[0], o[1], o[2]), mk(d[0], d[1], d[2]), seed, &segs, NULL, 0);
                 local += (unsigned long long)segs;
                 sx += r.x; sy += r.y; sz += r.z;
             }

@@ -122,6 +122,13 @@ void orc_render(const orc_scene* s, const orc_launch* lp, uint32_t first_frame, 
 /* one path (debug / per-sample parity) */
 void orc_sample_path(const orc_scene* s, const orc_launch* lp, int32_t x, int32_t y, uint32_t frame,
                      float out_rgb[3], int32_t* segments);
+/* The reference's debug pixel (devicePrograms.cu:637-644, printed at :428-437) as data: one path,
+ * ORC_DEBUG_FLOATS per shaded bounce (layout of ptamd.h pt_debug_bounce: bounce and prim as int32
+ * bits, position, albedo, shading normal, geometry normal, roughness, metallic, throughput
+ * entering the bounce, radiance before its NEE); returns the number of bounces recorded. */
+#define ORC_DEBUG_FLOATS 22
+int32_t orc_sample_path_debug(const orc_scene* s, const orc_launch* lp, int32_t x, int32_t y, uint32_t frame,
+                              float* records, int32_t max_bounces, float out_rgb[3]);
 
 #ifdef __cplusplus
 }
