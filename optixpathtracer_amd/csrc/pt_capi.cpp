@@ -163,6 +163,9 @@ struct pt_renderer {
         S.texels = d_texels;
         S.texinfo = d_texinfo;
         S.ntri = ntri;
+        S.n_nodes = bvh_nodes;
+        S.lds_nodes = nullptr;
+        S.n_lds = 0;
         return S;
     }
     float* accum() const { return user_accum ? user_accum : d_accum; }

@@ -38,6 +38,11 @@ struct DevScene {
     const uint32_t* texels;  // all textures' RGBA8 texels, concatenated
     const int4* texinfo;     // per texture: texel offset, width, height, 0
     int ntri;
+    int n_nodes;             // BVH4 nodes (breadth-first: the top levels are nodes 0 .. k)
+    // the first n_lds nodes staged in the workgroup's LDS by a trace kernel (stage_top_nodes);
+    // n_lds = 0 everywhere else
+    const BNode4* lds_nodes;
+    int n_lds;
 };
 
 // Material record (3 x float4 per mesh):
@@ -317,13 +322,25 @@ struct NodeLoad {
 };
 
 __device__ __forceinline__ NodeLoad node_load(const DevScene& S, const TravState& s, int ni) {
+    NodeLoad n;
+    if (ni < S.n_lds) {  // a top-level node staged in LDS (north_star: "BVH nodes ... staged through LDS")
+        const char* b = reinterpret_cast<const char*>(S.lds_nodes + ni);
+        auto ld = [&](int off) { return *reinterpret_cast<const float4*>(b + off); };
+        n.ax = ld(s.nx);
+        n.bx = ld(16 - s.nx);
+        n.ay = ld(32 + s.ny);
+        n.by = ld(48 - s.ny);
+        n.az = ld(64 + s.nz);
+        n.bz = ld(80 - s.nz);
+        n.ch = *reinterpret_cast<const int4*>(b + 96);
+        return n;
+    }
     // raw buffer loads: one 32-bit offset add per plane instead of a 64-bit address
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.nodes, 0, 0x7fffffff, 0x00020000);
     const int nb = ni << 7;
     auto ld = [&](int off) {
         return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + off, 0, 0));
     };
-    NodeLoad n;
     n.ax = ld(s.nx);
     n.bx = ld(16 - s.nx);
     n.ay = ld(32 + s.ny);
@@ -332,6 +349,20 @@ __device__ __forceinline__ NodeLoad node_load(const DevScene& S, const TravState
     n.bz = ld(80 - s.nz);
     n.ch = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + 96, 0, 0));
     return n;
+}
+
+// Copy the first min(n_nodes, K) BVH4 nodes (the top levels: nodes are numbered breadth-first)
+// into the workgroup's LDS and point the scene view at them.  Every thread of the block calls it
+// before any early exit.
+template <int K>
+__device__ __forceinline__ void stage_top_nodes(DevScene& S, BNode4* top) {
+    const int n = K > 0 ? min(S.n_nodes, K) : 0;
+    const float4* src = reinterpret_cast<const float4*>(S.nodes);
+    float4* dst = reinterpret_cast<float4*>(top);
+    for (int i = (int)threadIdx.x; i < n * 8; i += (int)blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    S.lds_nodes = top;
+    S.n_lds = n;
 }
 
 // Slab test of the four children of a loaded node, hits as (t_near, child) with misses and

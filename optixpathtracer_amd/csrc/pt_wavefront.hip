@@ -42,6 +42,12 @@ constexpr int kBlockWF = 256;
 #define PT_WF_STACK 16
 #endif
 constexpr int kStack = PT_WF_STACK;
+// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1; 85 = four full
+// levels, 10.9 KB: with the 16-KB stack a CU still holds 6 workgroups, above the VGPR limit of 5).
+#ifndef PT_LDS_NODES
+#define PT_LDS_NODES 85
+#endif
+constexpr int kLdsNodes = PT_LDS_NODES;
 #ifndef PT_WF_WAVES
 #define PT_WF_WAVES 1
 #endif
@@ -265,6 +271,8 @@ template <bool STATS, bool TEX>
 __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WFState W, int b, int dup,
                                                                   unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
+    __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    stage_top_nodes<kLdsNodes>(S, top);
     const int n = *cnt(W, b, kQueue);
     const int n_trace = n / dup;
     const float4* ro = W.ray_o[b & 1];
@@ -453,6 +461,8 @@ template <bool STATS, bool TEX>
 __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
+    __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    stage_top_nodes<kLdsNodes>(S, top);
     const int n_ext = *cnt(W, b + 1, kQueue);
     const int n_sh = *cnt(W, b, kShadowQ);
     const float4* ro = W.ray_o[(b + 1) & 1];
@@ -558,6 +568,8 @@ template <bool TEX>
 __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
+    __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    stage_top_nodes<kLdsNodes>(S, top);
     const int n = *cnt(W, b, kShadowQ);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[5], (unsigned long long)n);
     int* stk = stack + threadIdx.x;
