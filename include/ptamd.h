@@ -126,6 +126,16 @@ typedef struct pt_stats {
     uint64_t strict_retraces;    /* rays traced a second time because their first answer was a hit
                                     outside the triangle's own box (pt_device.h tri_accept; counted
                                     while pt_set_traversal_stats(r, 1)) */
+    /* wave schedule of the lane-refilling trace kernels (k_extend, k_trace_pair),
+       counted while pt_set_traversal_stats(r, 1): loop iterations of the waves, lanes with a ray
+       in flight summed over them, iterations that ran the node half / the triangle half of the
+       traversal step, and refill blocks.  nodes_visited / (64 * wave_node_steps) is the node
+       half's lane utilisation. */
+    uint64_t wave_steps;
+    uint64_t wave_active_lanes;
+    uint64_t wave_node_steps;
+    uint64_t wave_tri_steps;
+    uint64_t wave_refills;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;

@@ -115,6 +115,11 @@ class pt_stats(C.Structure):
         ("trace_kernel_rays", C.c_uint64),
         ("trace_kernel_bytes", C.c_uint64),
         ("strict_retraces", C.c_uint64),
+        ("wave_steps", C.c_uint64),
+        ("wave_active_lanes", C.c_uint64),
+        ("wave_node_steps", C.c_uint64),
+        ("wave_tri_steps", C.c_uint64),
+        ("wave_refills", C.c_uint64),
     ]
 
 

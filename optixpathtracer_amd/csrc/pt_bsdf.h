@@ -256,9 +256,6 @@ __device__ __forceinline__ float lambert_pdf(f3 wo, f3 wi, bool reflection) {
 }
 
 // ---- Dielectric (eta = 1.5): Dielectric.h:20-343 -------------------------------------------
-#ifndef PT_DIEL_CONVERGED
-#define PT_DIEL_CONVERGED 1  // rough dielectric sample: both lobes' shared terms computed once
-#endif
 enum { kRadiance = 0, kImportance = 1 };
 __device__ __forceinline__ float fresnel_dielectric(float cos_i, float ior) {  // :20-42
     cos_i = gclamp(cos_i, -1.0f, 1.0f);
@@ -359,7 +356,6 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
     if (!reflection) pr = 0.0f;
     if (!transmission) pt = 0.0f;
     if (pr == 0.0f && pt == 0.0f) return false;
-#if PT_DIEL_CONVERGED
     // The reflection and transmission branches (:162-236) run in the same wave whenever its
     // lanes draw different lobes (nearly always: R is a few percent).  Both branches evaluate
     // D(wm) and Lambda(wi) and end in the same divisions, so they are computed once here, on the
@@ -393,39 +389,6 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
     s.trans = !refl;
     s.spec = false;
     return true;
-#else
-    if (uc < pr / (pr + pt)) {
-        f3 I = -wo;  // glm::reflect(I, N) = I - N*dot(N,I)*2
-        float d = dot(wm, I);
-        f3 wi = mk(I.x - wm.x * d * 2.0f, I.y - wm.y * d * 2.0f, I.z - wm.z * d * 2.0f);
-        if (!same_hemisphere(wo, wi)) return false;
-        float pdf = p.g1c * tr_D(wm, alpha) * abs_dot(wo, wm) / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
-        float f = tr_D(wm, alpha) * (1.0f / (1.0f + p.lam + tr_lambda(wi, alpha))) * R / (4.0f * wi.z * wo.z);
-        s.color = mk(f, f, f);
-        s.dir = wi;
-        s.pdf = pdf;
-        s.refl = true;
-        s.trans = false;
-        s.spec = false;
-        return true;
-    }
-    float etap = 1.0f;
-    f3 wi = mk(0, 0, 0);
-    bool tir = !refract(wo, wm, eta, etap, wi);
-    if (tir || same_hemisphere(wo, wi) || wi.z == 0.0f) return false;
-    float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
-    float dwm_dwi = abs_dot(wi, wm) / denom;
-    float pdf = p.g1c * tr_D(wm, alpha) * abs_dot(wo, wm) * dwm_dwi * pt / (pr + pt);
-    float ft = T * tr_D(wm, alpha) * (1.0f / (1.0f + p.lam + tr_lambda(wi, alpha))) * fabsf(dot(wi, wm) * dot(wo, wm) / (wi.z * wo.z * denom));
-    if (mode == kRadiance) ft /= sqr(etap);
-    s.color = mk(ft, ft, ft);
-    s.dir = wi;
-    s.pdf = pdf;
-    s.refl = false;
-    s.trans = true;
-    s.spec = false;
-    return true;
-#endif
 }
 __device__ __forceinline__ bool dielectric_sample(uint32_t& seed, float roughness, f3 wo, BSample& s,
                                                   int mode, bool reflection, bool transmission) {
@@ -492,7 +455,6 @@ __device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, con
     const float G = 1.0f / (1.0f + po.lam + lam_i);
     const float tp = po.g1c * D * abs_dot(wo, wm);
     float fv, pv;
-#if PT_DIEL_CONVERGED
     // reflection and transmission in one sequence (lanes of a wave disagree on `reflect`): each
     // division takes its lobe's operands, so every value equals its branch's below
     const float R = F, T = 1.0f - R;
@@ -507,28 +469,6 @@ __device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, con
     const float qp = (reflect ? tp : abs_dot(wi, wm)) / (reflect ? 4.0f * abs_dot(wo, wm) : s2);
     pv = (reflect ? qp * pr : tp * qp * pt) / (pr + pt);
     if (pr == 0.0f && pt == 0.0f) pv = 0.0f;
-#else
-    if (reflect) {
-        fv = D * G * F / fabsf(4.0f * ci * co);
-    } else {
-        float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap) * ci * co;
-        fv = D * (1.0f - F) * G * fabsf(dot(wi, wm) * dot(wo, wm) / denom);
-        if (mode == kRadiance) fv /= sqr(etap);
-    }
-    const float R = F, T = 1.0f - R;
-    float pr = R, pt = T;
-    if (!reflection) pr = 0.0f;
-    if (!transmission) pt = 0.0f;
-    if (pr == 0.0f && pt == 0.0f) {
-        pv = 0.0f;
-    } else if (reflect) {
-        pv = tp / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
-    } else {
-        float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
-        float dwm_dwi = abs_dot(wi, wm) / denom;
-        pv = tp * dwm_dwi * pt / (pr + pt);
-    }
-#endif
     f = f_ok ? fv : 0.0f;
     pdf = p_ok ? pv : 0.0f;
 }
@@ -564,7 +504,7 @@ __device__ __forceinline__ bool layer_sample(bool top, uint32_t& seed, f3 albedo
 __device__ __forceinline__ float layer_pdf(bool top, float roughness, f3 wo, f3 wi, bool refl, bool trans) {
     return top ? dielectric_pdf(roughness, wo, wi, refl, trans) : lambert_pdf(wo, wi, refl);
 }
-// layer_f and layer_pdf of one interface at the same directions (PT_LAYERED_FUSE)
+// layer_f and layer_pdf of one interface at the same directions
 __device__ __forceinline__ void layer_f_pdf(bool top, f3 albedo, float roughness, f3 wo, f3 wi, int mode, bool refl,
                                             bool trans, f3& f, float& pdf) {
     if (top) {
@@ -584,21 +524,7 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
     return mk(b.color.x * c / b.pdf, b.color.y * c / b.pdf, b.color.z * c / b.pdf);
 }
 
-#ifndef PT_LAYERED_FUSE
-// 1: fused f + pdf per interface and hoisted transmittances; 2: + per-direction Trowbridge-Reitz
-// terms computed once (TRDir).  All levels give bit-identical results (tools/render_npy.py).
-#define PT_LAYERED_FUSE 2
-#endif
-#ifndef PT_LAYERED_INLINE
-#define PT_LAYERED_INLINE 0
-#endif
-#if PT_LAYERED_INLINE
-#define PT_LAYERED_ATTR __forceinline__
-#else
-#define PT_LAYERED_ATTR __noinline__
-#endif
-#if PT_LAYERED_FUSE >= 2
-__device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+__device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
     // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code).
     // The top interface is the rough or smooth dielectric, the bottom the Lambertian.  Terms
     // that depend on one direction only are computed once per direction (TRDir): wo and wi
@@ -738,125 +664,8 @@ __device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughne
     }
     return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
 }
-#else
-__device__ PT_LAYERED_ATTR f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
-    // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code)
-    const int mode = kRadiance;
-    const float thickness = 0.01f;
-    const bool topSpec = sqr(roughness) < 1e-3f;
-    const bool botSpec = false;
-    f3 f = mk(0, 0, 0);
-    if (wo.z < 0.0f) {
-        wo = -wo;
-        wi = -wi;
-    }
-    const bool enteredTop = true;
-    const bool same = same_hemisphere(wo, wi);
-    bool exitTop, nonExitTop, exitSpec, nonExitSpec;
-    if (same ^ enteredTop) {
-        exitSpec = botSpec; nonExitSpec = topSpec; exitTop = false; nonExitTop = true;
-    } else {
-        exitSpec = topSpec; nonExitSpec = botSpec; exitTop = true; nonExitTop = false;
-    }
-    const float exitZ = (same ^ enteredTop) ? 0.0f : thickness;
-    if (same) f = mk(5.0f, 5.0f, 5.0f) * layer_f(enteredTop, albedo, roughness, wo, wi, mode);
 
-    uint32_t ns = tea16(f2u_sat(wo.x * 1000.0f), f2u_sat(wo.y * 1000.0f));
-    ns = tea16(ns, f2u_sat(wi.x * 1000.0f));
-    ns = tea16(ns, f2u_sat(wi.y * 1000.0f));
-    ns = tea16(ns, seed);
-
-    for (int s = 0; s < 5; ++s) {
-        BSample wos, wis, bs;
-        bool ok = layer_sample(enteredTop, seed, albedo, roughness, wo, wos, mode, false, true);
-        if (bs_bad(ok, wos)) continue;
-        ok = layer_sample(exitTop, seed, albedo, roughness, wi, wis, kImportance, false, true);
-        if (bs_bad(ok, wis)) continue;
-        f3 beta = bs_weight(wos);
-        float z = enteredTop ? thickness : 0.0f;
-        f3 w = wos.dir;
-#if PT_LAYERED_FUSE
-        // loop-invariant / carried transmittances: the same calls on the same directions
-        const float tr_wis = transmittance(thickness, wis.dir);
-        float tr_w = transmittance(thickness, w);
-#endif
-        for (int depth = 0; depth < 10; ++depth) {
-            if (depth > 3 && save_max(beta) < 0.25f) {
-                float q = gmax(0.0f, 1.0f - save_max(beta));
-                if (rnd(ns) < q) break;
-                beta = beta / (1.0f - q);
-            }
-            z = (z == thickness) ? 0.0f : thickness;
-#if PT_LAYERED_FUSE
-            beta = beta * tr_w;
-#else
-            beta = beta * transmittance(thickness, w);
-#endif
-            // The reference branches on z == exitZ (GlossyDiffuse.h:315-360); lanes of a wave
-            // disagree on exitZ, so both branches would run every depth.  Here the two
-            // layer_sample calls are one call on the selected layer, with the NEE terms of the
-            // non-exit branch predicated around it: the same operations and random numbers.
-            // (Flattening the sample and depth loops into one loop of steps, so lanes start
-            // their next sample early, was 40 % slower: DESIGN.md §5.)
-            const bool atExit = z == exitZ;
-            if (!atExit && !nonExitSpec) {
-                float wt = 1.0f;
-#if PT_LAYERED_FUSE
-                f3 lf;
-                float lpdf;
-                layer_f_pdf(nonExitTop, albedo, roughness, -w, -wis.dir, mode, true, true, lf, lpdf);
-                if (!exitSpec) wt = power_heuristic(wis.pdf, lpdf);
-                const float tr = tr_wis;
-#else
-                if (!exitSpec)
-                    wt = power_heuristic(wis.pdf, layer_pdf(nonExitTop, roughness, -w, -wis.dir, true, true));
-                f3 lf = layer_f(nonExitTop, albedo, roughness, -w, -wis.dir, mode);
-                float tr = transmittance(thickness, wis.dir);
-#endif
-                float ac = abs_cos_theta(wis.dir);
-                f3 t1 = beta * lf;
-                t1 = t1 * ac;
-                t1 = t1 * wt;
-                t1 = t1 * tr;
-                t1 = t1 * wis.color;
-                t1 = t1 / wis.pdf;
-                f = f + t1;
-            }
-            ok = layer_sample(atExit ? exitTop : nonExitTop, seed, albedo, roughness, -w, bs, mode, true, false);
-            if (bs_bad(ok, bs)) break;
-            beta = beta * bs_weight(bs);
-            w = bs.dir;
-#if PT_LAYERED_FUSE
-            tr_w = transmittance(thickness, w);  // this NEE term's and the next depth's factor
-            if (!atExit && !exitSpec) {
-                f3 fExit;
-                float epdf;
-                layer_f_pdf(exitTop, albedo, roughness, -w, wi, mode, false, true, fExit, epdf);
-                if (!is_zero(fExit)) {
-                    float wt = 1.0f;
-                    if (!nonExitSpec) wt = power_heuristic(bs.pdf, epdf);
-                    const float tr = tr_w;
-#else
-            if (!atExit && !exitSpec) {
-                f3 fExit = layer_f(exitTop, albedo, roughness, -w, wi, mode);
-                if (!is_zero(fExit)) {
-                    float wt = 1.0f;
-                    if (!nonExitSpec) wt = power_heuristic(bs.pdf, layer_pdf(exitTop, roughness, -w, wi, false, true));
-                    float tr = transmittance(thickness, bs.dir);
-#endif
-                    f3 t1 = beta * tr;
-                    t1 = t1 * fExit;
-                    t1 = t1 * wt;
-                    f = f + t1;
-                }
-            }
-        }
-    }
-    return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
-}
-#endif
-
-__device__ PT_LAYERED_ATTR bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+__device__ __noinline__ bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
     // GlossyDiffuse.h:372-524
     const int mode = kRadiance;
     const float thickness = 0.01f;

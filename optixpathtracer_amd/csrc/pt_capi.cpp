@@ -84,7 +84,8 @@ struct EventPool {
 };
 
 // Device counters: [0] segments [1] nodes visited [2] triangle tests [3] rays [4] stack
-// overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces.
+// overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces
+// [9..13] wave schedule of the trace kernels (pt_stats wave_*).
 constexpr int kCounters = 16;
 constexpr int kMinTraversalStack = 16 + kSpillDepth;  // pt_wavefront.hip kStack + pt_device.h kSpillDepth
 
@@ -902,6 +903,11 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->trace_kernel_rays = c[6];
     out->trace_kernel_bytes = c[7];
     out->strict_retraces = c[8];
+    out->wave_steps = c[9];
+    out->wave_active_lanes = c[10];
+    out->wave_node_steps = c[11];
+    out->wave_tri_steps = c[12];
+    out->wave_refills = c[13];
     // a multi-device renderer reports the work of all its devices (times are device 0's)
     for (pt_renderer* p : r->peers) {
         pt_stats ps;
@@ -913,6 +919,11 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
         out->tri_tests += ps.tri_tests;
         out->rays += ps.rays;
         out->stack_overflows += ps.stack_overflows;
+        out->wave_steps += ps.wave_steps;
+        out->wave_active_lanes += ps.wave_active_lanes;
+        out->wave_node_steps += ps.wave_node_steps;
+        out->wave_tri_steps += ps.wave_tri_steps;
+        out->wave_refills += ps.wave_refills;
         out->shadow_rays += ps.shadow_rays;
         out->trace_kernel_rays += ps.trace_kernel_rays;
         out->trace_kernel_bytes += ps.trace_kernel_bytes;

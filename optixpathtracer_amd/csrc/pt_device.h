@@ -91,6 +91,9 @@ struct Hit {
 
 struct TravStats {
     uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0, retrace = 0;
+    // wave schedule (trace_range, lane 0 of each wave): iterations, active lanes summed over
+    // them, iterations running the node half / the triangle half, refill blocks
+    uint32_t steps = 0, active = 0, node_steps = 0, tri_steps = 0, refills = 0;
 };
 
 // ---- ray / box arithmetic shared bit for bit with the oracle ---------------------------------

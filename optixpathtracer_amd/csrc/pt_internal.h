@@ -40,7 +40,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
 struct WFState {
     float4* ray_o[2] = {nullptr, nullptr};  // queue b&1: origin.xyz | path id
     float4* ray_d[2] = {nullptr, nullptr};  // direction.xyz | 0
-    float4* hit = nullptr;                  // path (PT_HIT_PATH) or t, u, v, tri | back<<31 (-1 = miss), queue order
+    float4* hit = nullptr;                  // path, u, v, tri | back<<31 (-1 = miss), queue order
     float4* beta = nullptr;                 // path throughput.xyz | seed, path order
     float4* L = nullptr;                    // path radiance of the frame, path order
     float4* sh_o = nullptr;                 // shadow queue: origin | path

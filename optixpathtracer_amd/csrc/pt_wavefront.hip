@@ -77,12 +77,17 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
     if (!STATS || !counters) return;
     const unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
     const unsigned long long e = wave_sum_u64(ts.overflow), r = wave_sum_u64(ts.retrace);
-    if (lane_id() == 0) {
+    if (lane_id() == 0) {  // the wave-schedule counts are kept by every lane alike: lane 0's
         atomicAdd(&counters[1], a);
         atomicAdd(&counters[2], c);
         atomicAdd(&counters[3], d);
         atomicAdd(&counters[4], e);
         atomicAdd(&counters[8], r);
+        atomicAdd(&counters[9], (unsigned long long)ts.steps);
+        atomicAdd(&counters[10], (unsigned long long)ts.active);
+        atomicAdd(&counters[11], (unsigned long long)ts.node_steps);
+        atomicAdd(&counters[12], (unsigned long long)ts.tri_steps);
+        atomicAdd(&counters[13], (unsigned long long)ts.refills);
     }
 }
 
@@ -218,6 +223,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         // batch block once enough lanes idle (it costs the wave about as much as a step), and
         // at every step once the slice is drained
         if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
+            if (STATS) ts.refills++;
             if (done) {
                 if (trav_result_ok<ANY, TEX>(S, st)) {
                     finish(ri, st);
@@ -250,6 +256,12 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         const int n_leaf = __popcll(__ballot(active && st.leaf != kEmptyChild));
         const int n_node = __popcll(__ballot(active && st.cur >= 0));
         const bool tri_ok = n_leaf >= min(PT_TRI_BATCH, n_act) || 2 * n_node < n_act;
+        if (STATS) {
+            ts.steps++;
+            ts.active += n_act;
+            ts.node_steps += n_node > 0;
+            ts.tri_steps += tri_ok && n_leaf > 0;
+        }
         if (active && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts, tri_ok)) done = true;
     }
 }

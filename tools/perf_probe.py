@@ -75,6 +75,14 @@ def main():
                                     "tris_per_ray": round(s["tri_tests"] / rays, 2),
                                     "rays_per_sample": round(rays / (a.width * a.height * max(1, a.spp // 4)), 3),
                                     "stack_overflows": s["stack_overflows"]})
+                        ws = max(1, s["wave_steps"])
+                        out.update({"wave_steps_per_ray": round(s["wave_steps"] * 64 / rays, 2),
+                                    "active_frac": round(s["wave_active_lanes"] / (64 * ws), 3),
+                                    "node_util": round(s["nodes_visited"] / (64 * max(1, s["wave_node_steps"])), 3),
+                                    "tri_util": round(s["tri_tests"] / (64 * max(1, s["wave_tri_steps"])), 3),
+                                    "node_step_frac": round(s["wave_node_steps"] / ws, 3),
+                                    "tri_step_frac": round(s["wave_tri_steps"] / ws, 3),
+                                    "refill_frac": round(s["wave_refills"] / ws, 3)})
                     print(json.dumps(out), flush=True)
         r.close()
 
