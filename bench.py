@@ -247,15 +247,16 @@ def main():
             avg_launch_s = kernel_s / launches
             bytes_def = "396 B per segment + 12 B per sample"
         achieved = per_launch_bytes / avg_launch_s / 1e9
-        traffic = None
+        traffic = traffic_low = None
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
                 tjd = json.loads(tj.read_text())
                 if tjd.get("kernel") == dom and tjd.get("config", "2") == args.config:
                     traffic = tjd.get("hbm_bytes_per_launch")
+                    traffic_low = tjd.get("hbm_bytes_per_launch_low")
             except Exception:
-                traffic = None
+                traffic = traffic_low = None
         valu = None  # the VALU fraction beside the HBM roofline, from PMC passes
         vj = ROOT / "profiles" / "valu.json"
         if vj.exists() and dom == "k_extend+k_trace_pair" and args.config == "2":
@@ -313,6 +314,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic,
+                "traffic_low": traffic_low,
                 "kernel": dom,
                 "bytes_per_launch": int(per_launch_bytes),
                 "bytes_def": bytes_def,

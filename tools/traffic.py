@@ -4,9 +4,16 @@
     python tools/traffic.py PROFILE_DIR   (written by tools/profile.sh)
 
 FETCH_SIZE and WRITE_SIZE come from separate rocprofv3 runs.  Both are in KiB.  On gfx950
-FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled here.  WRITE_SIZE
-is exact for 16-B-per-lane stores.  These corrections follow MI355X_MICROARCH.md §HBM.  The
-result is written to profiles/traffic.json, where bench.py reads it for `roofline.traffic`.
+FETCH_SIZE reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM), so
+`hbm_bytes_per_launch` doubles it.  The calibration of tools/hbm_calib.hip
+(profiles/r02_hbm_calib.json) confirms the half count for streamed 16-B-per-lane reads and for
+runs of 24 records, but shows a random 16-B gather counted at 4x its payload (a line fetch per
+gather) with no evidence for doubling it, and WRITE_SIZE exact for streamed and window-shuffled
+16-B stores but 2x for random 16-B stores (32-B write granule).  The trace kernels mix streamed
+queue reads with gathers (W.L adds, BVH lines refetched from the Infinity Cache), so
+`hbm_bytes_per_launch_low` = FETCH_SIZE + WRITE_SIZE is reported beside it: the HBM bytes lie
+between the two.  The result is written to profiles/traffic.json, where bench.py reads it for
+`roofline.traffic` / `roofline.traffic_low`.
 """
 from __future__ import annotations
 
@@ -64,14 +71,17 @@ def main():
     f_kib = sum(fetch[kernel]) / len(fetch[kernel])
     w_kib = sum(write[kernel]) / len(write[kernel])
     hbm = 2.0 * f_kib * 1024.0 + w_kib * 1024.0
+    low = f_kib * 1024.0 + w_kib * 1024.0
     print(json.dumps({
         "kernel": kernel,
         "dispatches": len(fetch[kernel]),
         "fetch_size_kib_mean": round(f_kib, 3),
         "write_size_kib_mean": round(w_kib, 3),
         "hbm_bytes_per_launch": int(hbm),
+        "hbm_bytes_per_launch_low": int(low),
         "kernel_trace": stats.get(kernel),
-        "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes",
+        "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes; low: FETCH_SIZE + "
+                      "WRITE_SIZE (gathers are not half-counted, profiles/r02_hbm_calib.json)",
     }, indent=1))
 
 
