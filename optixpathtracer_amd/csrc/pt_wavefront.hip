@@ -120,10 +120,18 @@ constexpr int kWavesSh = kBlockSh / 64;
 #define PT_SHF_WAVES_OTHER 1
 #endif
 constexpr int shf_waves(int mode) { return (mode == 1 || mode == 3) /*Lambert, Dielectric*/ ? PT_SHF_WAVES : PT_SHF_WAVES_OTHER; }
-// k_shade_b (Default / Layered: the stochastic GlossyDiffuse eval + sample) needs more than
-// the 128 VGPRs a 1024-thread block allows, so it runs in smaller blocks.
+// k_shade_b (Default / Layered: the stochastic GlossyDiffuse eval + sample) runs in 256-thread
+// blocks at 4 waves per SIMD (128 VGPRs).  Its two phases are separated by a block barrier, and
+// a 1024-thread block (one per CU) held every SIMD slot of the CU while the waves without NEE
+// items waited at it; four independent 256-thread blocks per CU fill those slots with other
+// blocks' work: Layered 375 -> 433, Default 366 -> 408, Sponza-class 245 -> 258 Msamples/s
+// (1024 / 512 / 128 / 64 threads: 375 / 431 / 427 / 425 Layered; 168 VGPRs at 3 waves per SIMD:
+// 402).
 #ifndef PT_SHB_BLOCK
-#define PT_SHB_BLOCK 1024
+#define PT_SHB_BLOCK 256
+#endif
+#ifndef PT_SHB_WAVES
+#define PT_SHB_WAVES 4  // waves per SIMD the register allocator must allow (128 VGPRs)
 #endif
 constexpr int kBlockShB = PT_SHB_BLOCK;
 
@@ -632,7 +640,7 @@ __device__ __forceinline__ int block_bucket_scan(bool pred, bool bucket1, int* l
 // eval updates the path seed in W.beta before the sample reads it); only which thread works
 // on which path, and the order of the appends to the next queue, change.
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockShB) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+__global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     constexpr int kW = kBlockShB / 64;
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
