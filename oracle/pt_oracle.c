@@ -1010,7 +1010,21 @@ static int alpha_cut(const orc_scene* s, int t, float u, float v) {
  * this binary median split agree bit for bit).  Without the rule a grazing ray could be
  * accepted at a point outside the triangle's own box and the answer depended on which
  * triangle set `best` first (one trace in 62 M of the config-5 band). */
+/* The traversal and the path loop are compiled twice, with and without the FMA instruction set,
+ * and the loader picks the FMA clone where the CPU has it: fmaf is then one instruction instead
+ * of a libm call.  fmaf is exactly rounded either way, so both clones give the same bits. */
+#if defined(__x86_64__) && defined(__GNUC__)
+#define ORC_HOT __attribute__((target_clones("fma", "default")))
+#else
+#define ORC_HOT
+#endif
 static const float kSlabWiden = 1.000244140625f;
+/* fminf / fmaxf without the libm call (gcc calls them unless NaNs and signed zeros are
+ * excluded, and the traversal spent most of its time there).  No NaN reaches these: slab
+ * distances are fmaf(plane, inv, -o*inv) with finite inv (a zero direction component maps to
+ * +-1e30), and which zero a tie returns does not change a comparison or a padded box. */
+static inline float mn(float a, float b) { return b < a ? b : a; }
+static inline float mx(float a, float b) { return b > a ? b : a; }
 static inline float ray_inv(float d) { return d != 0.0f ? 1.0f / d : copysignf(1e30f, d); }
 static inline float box_pad(float x) { return fabsf(x) * 9.5367431640625e-7f + 1e-6f; }
 static void tri_bounds(const orc_scene* s, int t, float lo[3], float hi[3]) {
@@ -1018,7 +1032,7 @@ static void tri_bounds(const orc_scene* s, int t, float lo[3], float hi[3]) {
     float a[3] = {v0.x, v0.y, v0.z}, b[3] = {e1.x, e1.y, e1.z}, c[3] = {e2.x, e2.y, e2.z};
     for (int k = 0; k < 3; ++k) {
         float p1 = a[k] + b[k], p2 = a[k] + c[k];
-        float l = fminf(fminf(a[k], p1), p2), h = fmaxf(fmaxf(a[k], p1), p2);
+        float l = mn(mn(a[k], p1), p2), h = mx(mx(a[k], p1), p2);
         lo[k] = l - box_pad(l);
         hi[k] = h + box_pad(h);
     }
@@ -1028,8 +1042,8 @@ static inline void slab_interval(const float lo[3], const float hi[3], v3 inv, v
     float ax = fmaf(lo[0], inv.x, -io.x), bx = fmaf(hi[0], inv.x, -io.x);
     float ay = fmaf(lo[1], inv.y, -io.y), by = fmaf(hi[1], inv.y, -io.y);
     float az = fmaf(lo[2], inv.z, -io.z), bz = fmaf(hi[2], inv.z, -io.z);
-    *tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-    *tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    *tn = mx(mx(mn(ax, bx), mn(ay, by)), mn(az, bz));
+    *tf = mn(mn(mx(ax, bx), mx(ay, by)), mx(az, bz));
 }
 static int tri_accept(const orc_scene* s, int t, v3 inv, v3 io, float th) {
     float lo[3], hi[3], tn, tf;
@@ -1178,7 +1192,7 @@ static int tri_hit(const orc_scene* s, int t, v3 o, v3 d, float tmin, float tmax
 static int box_hit(const onode* nd, v3 inv, v3 io, float tmin, float tmax) {
     float tn, tf;
     slab_interval(nd->lo, nd->hi, inv, io, &tn, &tf);
-    return fmaxf(tn, tmin) <= fminf(tf, tmax) * kSlabWiden;
+    return mx(tn, tmin) <= mn(tf, tmax) * kSlabWiden;
 }
 static int trace_impl(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int anyhit, float* th,
                       float* uh, float* vh, int* back, int cull);
@@ -1222,8 +1236,8 @@ static int trace(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int any
     if (r >= 0 && th) { *th = t0; *uh = u0; *vh = v0; *back = b0; }
     return r;
 }
-static int trace_impl(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int anyhit, float* th,
-                      float* uh, float* vh, int* back, int cull) {
+ORC_HOT static int trace_impl(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, int anyhit, float* th,
+                              float* uh, float* vh, int* back, int cull) {
     if (s->ntri == 0) return -1;
     v3 inv = mk(ray_inv(d.x), ray_inv(d.y), ray_inv(d.z));
     v3 io = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
@@ -1271,7 +1285,7 @@ int32_t orc_trace_any(const orc_scene* s, const float o[3], const float d[3], fl
 /* ------------------------------------------------------------------------------------ */
 /* The path — SamplePath (devicePrograms.cu:625-664) + __closesthit__radiance (:343-514)  */
 /* ------------------------------------------------------------------------------------ */
-static v3 sample_path(const orc_scene* s, const orc_launch* lp, v3 origin, v3 dir, uint32_t seed,
+ORC_HOT static v3 sample_path(const orc_scene* s, const orc_launch* lp, v3 origin, v3 dir, uint32_t seed,
                       int* segs, float* dbg, int dbg_max) {
     v3 radiance = mk(0, 0, 0), beta = mk(1, 1, 1);
     int bounce = 0, endPath = 0;
