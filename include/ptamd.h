@@ -222,6 +222,16 @@ int pt_set_accum_device_buffer(pt_renderer* r, float* device_sum_rgb);
 float* pt_accum_device_ptr(pt_renderer* r);
 /* Download the sum (scale = 1) or the mean (scale = 1/spp) to host. */
 int pt_accum_download(pt_renderer* r, float* host_rgb, float scale);
+/* fp64 accumulation (off by default: the reference's sum is fp32, OptixView.cpp:232-245).  On:
+ * every sample's fp32 radiance is added in fp64 and the fp32 sum buffer holds the fp64 sum
+ * rounded to fp32; a multi-device renderer reduces the devices' fp64 sums (ncclFloat64), so the
+ * image no longer depends on how the frame ids were split over devices (up to fp64 rounding,
+ * ~1e-16 relative, which the final rounding to fp32 almost always absorbs).  Switching it on
+ * starts from the current fp32 sum.  Wavefront kernel only (PT_KERNEL_AUTO resolves to it);
+ * a megakernel render returns PT_ERR_INVALID. */
+int pt_set_accum_fp64(pt_renderer* r, int32_t on);
+double* pt_accum_device_ptr64(pt_renderer* r);  /* NULL while off */
+int pt_accum_download64(pt_renderer* r, double* host_rgb);
 
 /* Waits for every device of the renderer. */
 int pt_synchronize(pt_renderer* r);

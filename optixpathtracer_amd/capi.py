@@ -168,6 +168,9 @@ SIGNATURES = {
     "pt_set_accum_device_buffer": (C.c_int, [_R, C.c_void_p]),
     "pt_accum_device_ptr": (C.c_void_p, [_R]),
     "pt_accum_download": (C.c_int, [_R, _FP, C.c_float]),
+    "pt_set_accum_fp64": (C.c_int, [_R, C.c_int32]),
+    "pt_accum_device_ptr64": (C.c_void_p, [_R]),
+    "pt_accum_download64": (C.c_int, [_R, C.POINTER(C.c_double)]),
     "pt_synchronize": (C.c_int, [_R]),
     "pt_stream": (C.c_void_p, [_R]),
     "pt_device_count": (C.c_int32, [_R]),

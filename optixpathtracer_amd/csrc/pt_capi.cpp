@@ -149,6 +149,11 @@ struct pt_renderer {
     std::vector<pt_renderer*> peers;
     std::vector<ncclComm_t> comms;
     float* d_part = nullptr;  // device 0's own partial sum (the total is accum())
+    // pt_set_accum_fp64: the sum is kept in fp64 (d_accum64; device 0 of a multi-device renderer
+    // also d_part64), accum() holds its fp32 rounding
+    bool accum64 = false;
+    double* d_accum64 = nullptr;
+    double* d_part64 = nullptr;
     // debug path (pt_set_debug_pixel): pixel W*y+x (-1 = off), frame id, per-bounce records
     int debug_pixel = -1;
     uint32_t debug_frame = 0;
@@ -194,7 +199,8 @@ int next_event_pair(pt_renderer* r, hipEvent_t* a, hipEvent_t* b) {
     return PT_OK;
 }
 
-DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, uint32_t n_frames) {
+DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, uint32_t n_frames,
+                      double* accum64 = nullptr) {
     DevLaunch L;
     L.width = r->width;
     L.height = r->height;
@@ -207,6 +213,7 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
     L.frame_base = frame_base;
     L.n_frames = n_frames;
     L.accum = accum;
+    L.accum64 = accum64;
     L.counters = r->d_counters;
     L.debug_pixel = r->d_debug ? r->debug_pixel : -1;
     L.debug_frame = r->debug_frame;
@@ -217,7 +224,7 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
 // Launch frames [first, first+n) in chunks, adding into accum; brackets with events.  Does not
 // wait for earlier work: the event pairs of every launch since the last synchronisation point
 // are summed at the next pt_synchronize / pt_get_stats / download (collect_pending).
-int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
+int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, double* accum64 = nullptr) {
     int rc = PT_OK;
     const DevScene S = r->scene();
     uint32_t done = 0;
@@ -228,6 +235,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
     // Dielectric 1239 / 758, Default 255 / 104).
     int kernel = r->kernel;
     if (kernel == PT_KERNEL_AUTO) kernel = PT_KERNEL_WAVEFRONT;
+    if (accum64 && kernel != PT_KERNEL_WAVEFRONT)
+        return fail(PT_ERR_INVALID, "fp64 accumulation (pt_set_accum_fp64) runs with the wavefront kernel");
     if (kernel == PT_KERNEL_WAVEFRONT) {
         // Frames per wavefront launch chain: the queues hold nf frames' paths (168 B each), at most
         // kMaxWFPaths of them.  Batching amortises launch gaps and the per-kernel SIMT tail:
@@ -245,7 +254,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n) {
         (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, r->device);
         for (uint32_t f = 0; f < n;) {  // one event pair per batch (the batch's kernel chain)
             const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
-            DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf);
+            DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf, accum64);
             hipEvent_t a, b;
             rc = next_event_pair(r, &a, &b);
             if (rc) return rc;
@@ -302,7 +311,8 @@ int render_frames_multi(pt_renderer* r, uint32_t first, uint32_t n) {
         pt_renderer* d = g == 0 ? r : r->peers[(size_t)g - 1];
         if (ng > 0) {
             PT_HIP(hipSetDevice(d->device), "hipSetDevice");
-            const int rc = launch_frames(d, g == 0 ? r->d_part : d->accum(), f, ng);
+            const int rc = launch_frames(d, g == 0 ? r->d_part : d->accum(), f, ng,
+                                         r->accum64 ? (g == 0 ? r->d_part64 : d->d_accum64) : nullptr);
             if (rc) return rc;
         }
         f += ng;
@@ -310,14 +320,36 @@ int render_frames_multi(pt_renderer* r, uint32_t first, uint32_t n) {
     ncclResult_t nr = ncclGroupStart();
     for (int g = 0; g < N && nr == ncclSuccess; ++g) {
         pt_renderer* d = g == 0 ? r : r->peers[(size_t)g - 1];
-        const float* send = g == 0 ? r->d_part : d->accum();
-        float* recv = g == 0 ? r->accum() : d->accum();  // significant on the root only
-        nr = ncclReduce(send, recv, count, ncclFloat32, ncclSum, 0, r->comms[(size_t)g], d->stream);
+        if (r->accum64) {  // fp64 partial sums -> fp64 total on device 0
+            const double* send = g == 0 ? r->d_part64 : d->d_accum64;
+            double* recv = g == 0 ? r->d_accum64 : d->d_accum64;  // significant on the root only
+            nr = ncclReduce(send, recv, count, ncclFloat64, ncclSum, 0, r->comms[(size_t)g], d->stream);
+        } else {
+            const float* send = g == 0 ? r->d_part : d->accum();
+            float* recv = g == 0 ? r->accum() : d->accum();  // significant on the root only
+            nr = ncclReduce(send, recv, count, ncclFloat32, ncclSum, 0, r->comms[(size_t)g], d->stream);
+        }
     }
     const ncclResult_t ne = ncclGroupEnd();
     (void)hipSetDevice(r->device);
     if (nr != ncclSuccess || ne != ncclSuccess)
         return fail(PT_ERR_HIP, std::string("ncclReduce: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ne));
+    if (r->accum64) PT_HIP(accum_f64_to_f32(r->d_accum64, r->accum(), count, r->stream), "fp64 -> fp32 sum");
+    return PT_OK;
+}
+
+// fp64 sum buffers (pt_set_accum_fp64) of one device for a W x H image, zeroed
+int alloc_accum64(pt_renderer* r, int width, int height) {
+    const size_t bytes = sizeof(double) * 3 * (size_t)width * (size_t)height;
+    if (r->d_accum64) (void)hipFree(r->d_accum64);
+    if (r->d_part64) (void)hipFree(r->d_part64);
+    r->d_accum64 = r->d_part64 = nullptr;
+    PT_HIP(hipMalloc(&r->d_accum64, bytes), "hipMalloc fp64 accum");
+    PT_HIP(hipMemsetAsync(r->d_accum64, 0, bytes, r->stream), "hipMemset fp64 accum");
+    if (!r->comms.empty()) {
+        PT_HIP(hipMalloc(&r->d_part64, bytes), "hipMalloc fp64 partial sum");
+        PT_HIP(hipMemsetAsync(r->d_part64, 0, bytes, r->stream), "hipMemset fp64 partial sum");
+    }
     return PT_OK;
 }
 
@@ -577,6 +609,8 @@ int pt_destroy(pt_renderer* r) {
     for (pt_renderer* p : r->peers) pt_destroy(p);
     (void)hipSetDevice(r->device);
     if (r->d_part) (void)hipFree(r->d_part);
+    if (r->d_part64) (void)hipFree(r->d_part64);
+    if (r->d_accum64) (void)hipFree(r->d_accum64);
     (void)hipSetDevice(r->device);
     if (r->d_nodes) (void)hipFree(r->d_nodes);
     if (r->d_isect) (void)hipFree(r->d_isect);
@@ -614,7 +648,10 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_display) (void)hipFree(r->d_display);
     if (r->d_part) (void)hipFree(r->d_part);
+    if (r->d_accum64) (void)hipFree(r->d_accum64);
+    if (r->d_part64) (void)hipFree(r->d_part64);
     r->d_frame = r->d_accum = r->d_display = r->d_part = nullptr;
+    r->d_accum64 = r->d_part64 = nullptr;
     r->display_ready = false;
     // the size is committed only once every buffer exists (a failed allocation leaves an
     // unsized renderer, on which the render calls return PT_ERR_STATE)
@@ -626,6 +663,10 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
     if (!r->comms.empty()) {
         PT_HIP(hipMalloc(&r->d_part, bytes), "hipMalloc partial sum");
         PT_HIP(hipMemsetAsync(r->d_part, 0, bytes, r->stream), "hipMemset partial sum");
+    }
+    if (r->accum64) {
+        const int rc = alloc_accum64(r, width, height);
+        if (rc) return rc;
     }
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     r->width = width;
@@ -806,6 +847,8 @@ int pt_accum_clear(pt_renderer* r) {
     size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
     PT_HIP(hipMemsetAsync(r->accum(), 0, bytes, r->stream), "hipMemset accum");
     if (r->d_part) PT_HIP(hipMemsetAsync(r->d_part, 0, bytes, r->stream), "hipMemset partial sum");
+    if (r->d_accum64) PT_HIP(hipMemsetAsync(r->d_accum64, 0, 2 * bytes, r->stream), "hipMemset fp64 accum");
+    if (r->d_part64) PT_HIP(hipMemsetAsync(r->d_part64, 0, 2 * bytes, r->stream), "hipMemset fp64 partial sum");
     return PT_OK;
 }
 
@@ -814,7 +857,8 @@ int pt_render_frames(pt_renderer* r, uint32_t first_frame_id, uint32_t n_frames)
     if (r->width == 0) return fail(PT_ERR_STATE, "pt_render_frames: call pt_resize first");
     if (n_frames == 0) return PT_OK;
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
-    if (r->comms.empty()) return launch_frames(r, r->accum(), first_frame_id, n_frames);
+    if (r->comms.empty())
+        return launch_frames(r, r->accum(), first_frame_id, n_frames, r->accum64 ? r->d_accum64 : nullptr);
     return render_frames_multi(r, first_frame_id, n_frames);
 }
 
@@ -837,6 +881,50 @@ int pt_set_accum_device_buffer(pt_renderer* r, float* device_sum_rgb) {
 }
 
 float* pt_accum_device_ptr(pt_renderer* r) { return r ? r->accum() : nullptr; }
+
+int pt_set_accum_fp64(pt_renderer* r, int32_t on) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_accum_fp64: NULL");
+    for (pt_renderer* p : r->peers) {
+        const int rc = pt_set_accum_fp64(p, on);
+        if (rc) return rc;
+    }
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    r->accum64 = on != 0;
+    if (r->accum64 && r->width > 0) {
+        // start from the current fp32 sum (device 0 of a multi-device renderer: its own partial
+        // sum, which the next reduce adds to the others'), so a switch keeps what is there
+        const int rc = alloc_accum64(r, r->width, r->height);
+        if (rc) return rc;
+        const size_t n = 3 * (size_t)r->width * (size_t)r->height;
+        std::vector<float> h32(n);
+        std::vector<double> h64(n);
+        const float* src = r->comms.empty() ? r->accum() : r->d_part;
+        double* dst = r->comms.empty() ? r->d_accum64 : r->d_part64;
+        PT_HIP(hipMemcpy(h32.data(), src, n * sizeof(float), hipMemcpyDeviceToHost), "download accum");
+        for (size_t i = 0; i < n; ++i) h64[i] = (double)h32[i];
+        PT_HIP(hipMemcpy(dst, h64.data(), n * sizeof(double), hipMemcpyHostToDevice), "upload fp64 accum");
+    } else if (!r->accum64) {
+        if (r->d_accum64) (void)hipFree(r->d_accum64);
+        if (r->d_part64) (void)hipFree(r->d_part64);
+        r->d_accum64 = r->d_part64 = nullptr;
+    }
+    return PT_OK;
+}
+
+double* pt_accum_device_ptr64(pt_renderer* r) { return r ? r->d_accum64 : nullptr; }
+
+int pt_accum_download64(pt_renderer* r, double* host_rgb) {
+    if (!r || !host_rgb) return fail(PT_ERR_INVALID, "pt_accum_download64: NULL");
+    if (r->width == 0) return fail(PT_ERR_STATE, "pt_accum_download64: call pt_resize first");
+    if (!r->d_accum64) return fail(PT_ERR_STATE, "pt_accum_download64: fp64 accumulation is off (pt_set_accum_fp64)");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    size_t n = 3 * (size_t)r->width * (size_t)r->height;
+    PT_HIP(hipMemcpyAsync(host_rgb, r->d_accum64, n * sizeof(double), hipMemcpyDeviceToHost, r->stream),
+           "download fp64 accum");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    return collect_pending(r);
+}
 
 int pt_accum_download(pt_renderer* r, float* host_rgb, float scale) {
     if (!r || !host_rgb) return fail(PT_ERR_INVALID, "pt_accum_download: NULL");

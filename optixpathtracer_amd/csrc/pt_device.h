@@ -65,6 +65,8 @@ struct DevLaunch {
     uint32_t frame_base;
     uint32_t n_frames;
     float* accum;                    // W*H*3 fp32 sum
+    double* accum64;                 // pt_set_accum_fp64: W*H*3 fp64 sum (accum then holds its
+                                     // fp32 rounding); NULL = fp32 accumulation
     unsigned long long* counters;    // [0] segments [1] nodes visited [2] triangle tests [3] rays
     // debug path (pt_set_debug_pixel; the reference's isDebugRay, devicePrograms.cu:637-644):
     // the path of pixel debug_pixel (W*y + x, -1 = off) at frame debug_frame records every

@@ -53,6 +53,8 @@ struct WFState {
     int max_bounces = 0;
 };
 size_t wavefront_bytes(int paths, int max_bounces);
+// sum32[i] = (float)sum64[i] (the multi-device fp64 reduce's result -> the fp32 sum buffer)
+hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStream_t stream);
 hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces);
 void wavefront_free(WFState& W);
 // Enqueue one frame (all bounces) of the wavefront pipeline; adds the frame into L.accum.

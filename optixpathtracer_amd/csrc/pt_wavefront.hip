@@ -730,6 +730,22 @@ __global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L, int 
     const int P = L.width * L.height;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
         const size_t idx = (size_t)p * 3;
+        if (L.accum64) {  // pt_set_accum_fp64: the frames' fp32 radiance summed in fp64
+            double sx = L.accum64[idx], sy = L.accum64[idx + 1], sz = L.accum64[idx + 2];
+            for (int f = 0; f < nf; ++f) {
+                const float4 l = W.L[(size_t)f * P + p];
+                sx += (double)l.x;
+                sy += (double)l.y;
+                sz += (double)l.z;
+            }
+            L.accum64[idx] = sx;
+            L.accum64[idx + 1] = sy;
+            L.accum64[idx + 2] = sz;
+            L.accum[idx] = (float)sx;
+            L.accum[idx + 1] = (float)sy;
+            L.accum[idx + 2] = (float)sz;
+            continue;
+        }
         float sx = L.accum[idx], sy = L.accum[idx + 1], sz = L.accum[idx + 2];
         for (int f = 0; f < nf; ++f) {  // frames in order: the sequential accumulation
             const float4 l = W.L[(size_t)f * P + p];
@@ -741,6 +757,11 @@ __global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L, int 
         L.accum[idx + 1] = sy;
         L.accum[idx + 2] = sz;
     }
+}
+
+__global__ __launch_bounds__(kBlockWF) void k_f64_to_f32(const double* __restrict__ a, float* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        b[i] = (float)a[i];
 }
 
 inline bool fused_mode(int mode) { return mode == kModeLambert || mode == kModeConductor || mode == kModeDielectric; }
@@ -803,6 +824,12 @@ hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevL
 }
 
 }  // namespace
+
+hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStream_t stream) {
+    const unsigned blocks = (unsigned)std::min<size_t>((n + kBlockWF - 1) / kBlockWF, 8192);
+    hipLaunchKernelGGL(k_f64_to_f32, dim3(std::max(1u, blocks)), dim3(kBlockWF), 0, stream, sum64, sum32, n);
+    return hipGetLastError();
+}
 
 size_t wavefront_bytes(int paths, int max_bounces) {
     size_t P = (size_t)paths;

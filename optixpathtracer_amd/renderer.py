@@ -221,6 +221,17 @@ class OptixRenderer:
         check(self.lib.pt_accum_download(self.h, fptr(out), float(scale)), "pt_accum_download")
         return out
 
+    def set_accum_fp64(self, enable: bool) -> None:
+        """pt_set_accum_fp64: add the samples in fp64 (accum() then returns the fp64 sum rounded
+        to fp32, accum64() the fp64 sum); off by default (the reference sums in fp32)."""
+        check(self.lib.pt_set_accum_fp64(self.h, 1 if enable else 0), "pt_set_accum_fp64")
+
+    def accum64(self) -> np.ndarray:
+        w, h = self.size
+        out = np.empty((h, w, 3), np.float64)
+        check(self.lib.pt_accum_download64(self.h, out.ctypes.data_as(C.POINTER(C.c_double))), "pt_accum_download64")
+        return out
+
     def synchronize(self) -> None:
         check(self.lib.pt_synchronize(self.h), "pt_synchronize")
 
