@@ -520,6 +520,141 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, TravState& s, int* 
     return s.cur == kEmptyChild && s.leaf == kEmptyChild;
 }
 
+// ---- wave-batched triangle tests (the lane-refilling wavefront trace loop) -----------------
+// The triangle half of the per-lane step (trav_step) tests one triangle of a lane's leaf per
+// step, and only about a third of the lanes hold a leaf when it runs (DESIGN.md §4 "Wave
+// schedule").  Here the wave instead lists every triangle of every pending leaf as (triangle,
+// owner lane) pairs in LDS and tests them 64 at a time, each lane taking one pair and fetching
+// the owner's ray with cross-lane reads.  A pair's hit competes for its owner by the key
+// (t, original index) -- t >= 0, so its bits order as an unsigned integer -- through an LDS
+// 64-bit atomic min; the owner then takes the winner by the closest-hit rule of leaf_tri_eval.
+// The answer is the same (t, index) minimum over acceptable hits as in trav_step.
+constexpr int kTriPairsPerWave = 256;  // 64 lanes x <= 4 triangles per leaf
+struct TriBatchLds {                    // one per wave
+    uint32_t pair[kTriPairsPerWave];    // (leaf-order triangle << 6) | owner lane
+    unsigned long long key[64];         // per owner: min over this round's hits of (t bits << 32 | orig)
+    float4 res[64];                     // per owner: the winning pair's u, v, tri | back << 31
+};
+
+__device__ __forceinline__ int lane_prefix(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Every lane of the wave calls this (wave-uniform control flow); `has` = the lane holds a
+// pending leaf.  Tests all those leaves' triangles, empties the leaf slots and updates the
+// owners' hits.  The trace loop's rays have tmin = 0.
+template <int ANY, bool STATS, bool TEX>
+__device__ __forceinline__ void wave_tri_batch(const DevScene& S, TravState& s, bool has, TriBatchLds* L,
+                                               TravStats& ts) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int c1 = has ? leaf_count(s.leaf) - 1 : 0;  // 0..3
+    const int first = leaf_first(s.leaf);
+    const unsigned long long m0 = __ballot(has), m1 = __ballot(has && (c1 & 1)), m2 = __ballot(has && (c1 & 2));
+    const int pre = lane_prefix(m0) + lane_prefix(m1) + 2 * lane_prefix(m2);
+    const int total = (int)(__popcll(m0) + __popcll(m1) + 2 * __popcll(m2));
+    if (has) {
+        L->pair[pre] = ((uint32_t)first << 6) | (uint32_t)lane;
+        if (c1 >= 1) L->pair[pre + 1] = ((uint32_t)(first + 1) << 6) | (uint32_t)lane;
+        if (c1 >= 2) L->pair[pre + 2] = ((uint32_t)(first + 2) << 6) | (uint32_t)lane;
+        if (c1 >= 3) L->pair[pre + 3] = ((uint32_t)(first + 3) << 6) | (uint32_t)lane;
+        s.leaf = kEmptyChild;
+    }
+    L->key[lane] = ~0ull;
+    const int flags = (s.strict ? 1 : 0) | (is_any<ANY>(s) ? 2 : 0);
+    const bool any_strict = __ballot(has && s.strict) != 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int base = 0; base < total; base += 64) {  // total is wave-uniform
+        const int k = base + lane;
+        const bool valid = k < total;
+        const uint32_t pair = L->pair[valid ? k : 0];
+        const int owner = (int)(pair & 63u), ti = (int)(pair >> 6);
+        const f3 o = mk(__shfl(s.o.x, owner, 64), __shfl(s.o.y, owner, 64), __shfl(s.o.z, owner, 64));
+        const f3 d = mk(__shfl(s.d.x, owner, 64), __shfl(s.d.y, owner, 64), __shfl(s.d.z, owner, 64));
+        const float tmax = __shfl(s.best, owner, 64);
+        const int fl = __shfl(flags, owner, 64);
+        bool hit = false, bk = false;
+        float t = 0.0f, u = 0.0f, v = 0.0f;
+        int oi = 0;
+        if (valid) {
+            if (STATS) ts.tris++;
+            const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+            hit = tri_test(A, E1, E2, o, d, 0.0f, tmax, t, u, v, bk);
+            if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
+            if (any_strict && (fl & 1) && hit) {  // re-trace lanes only (rare): the owner's inv / io, recomputed
+                const f3 inv = safe_inv(d);
+                hit = tri_accept(A, E1, E2, inv, mk(o.x * inv.x, o.y * inv.y, o.z * inv.z), t);
+            }
+            oi = __float_as_int(A.w);
+        }
+        // t >= tmin = 0: with the sign bit cleared (t = -0), its bits order as an unsigned integer
+        const unsigned long long key =
+            ((unsigned long long)(__float_as_uint(t) & 0x7fffffffu) << 32) | (unsigned long long)(uint32_t)oi;
+        if (hit) atomicMin(&L->key[owner], key);
+        __builtin_amdgcn_wave_barrier();
+        if (hit && L->key[owner] == key)  // the owner's winning pair (a triangle is in one leaf only)
+            L->res[owner] = make_float4(u, v, __int_as_float(ti | (bk ? (int)0x80000000 : 0)), 0.0f);
+        __builtin_amdgcn_wave_barrier();
+        const unsigned long long w = L->key[lane];
+        if (w != ~0ull) {
+            const float tw = __uint_as_float((uint32_t)(w >> 32));
+            const int ow = (int)(uint32_t)w;
+            const float4 r = L->res[lane];
+            const int code = __float_as_int(r.z);
+            if (flags & 2) {  // (this lane's own kind) any hit: done; only h.tri (the record's other fields carry the path)
+                s.h.tri = code & 0x7fffffff;
+                s.path = __float_as_int(tw);
+            } else if (tw < s.best || (tw == s.best && ow < s.h.orig)) {
+                s.best = tw;
+                s.h.t = tw;
+                s.h.u = r.x;
+                s.h.v = r.y;
+                s.h.tri = code & 0x7fffffff;
+                s.h.back = code < 0;
+                s.h.orig = ow;
+            }
+            L->key[lane] = ~0ull;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// The node half and hand-off of trav_step (the wavefront loop tests triangles in wave batches).
+template <int ANY, bool STATS, int DEPTH>
+__device__ __forceinline__ bool trav_node_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
+                                               int* spill, TravStats& ts) {
+    if (s.cur >= 0) {
+        if (STATS) ts.nodes++;
+        float t0, t1, t2, t3;
+        int c0, c1, c2, c3;
+        node_eval(node_load(S, s, s.cur), s, t0, t1, t2, t3, c0, c1, c2, c3);
+        if (ANY != kRayAny) {
+            cswap(t0, c0, t1, c1);
+            cswap(t2, c2, t3, c3);
+            cswap(t0, c0, t2, c2);
+            cswap(t1, c1, t3, c3);
+            cswap(t1, c1, t2, c2);
+        }
+        if (s.sp > DEPTH - 3) stack_spill<DEPTH, STATS>(s, stk, stride, spill, ts);
+        {
+            int sp = s.sp;
+            stk[sp * stride] = c3;
+            sp += c3 != kEmptyChild;
+            stk[sp * stride] = c2;
+            sp += c2 != kEmptyChild;
+            stk[sp * stride] = c1;
+            sp += c1 != kEmptyChild;
+            s.sp = sp;
+        }
+        s.cur = c0;
+    }
+    if (s.cur == kEmptyChild) stack_pop<DEPTH>(s, stk, stride, spill);
+    if (s.cur < 0 && s.cur != kEmptyChild && s.leaf == kEmptyChild) {
+        s.leaf = s.cur;
+        stack_pop<DEPTH>(s, stk, stride, spill);
+    }
+    return s.cur == kEmptyChild && s.leaf == kEmptyChild;
+}
+
 // A finished traversal's answer stands unless its hit is not acceptable (tri_accept) -- then
 // the ray is traced again in strict mode.  If the final hit is acceptable it IS the minimum
 // over the acceptable hits: every acceptable hit ordered before it had t <= best throughout,

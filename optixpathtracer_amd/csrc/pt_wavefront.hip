@@ -42,15 +42,23 @@ constexpr int kBlockWF = 256;
 #define PT_WF_STACK 16
 #endif
 constexpr int kStack = PT_WF_STACK;
-// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1; 85 = four full
-// levels, 10.9 KB: with the 16-KB stack a CU still holds 6 workgroups, above the VGPR limit of 5).
+// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 41 =
+// the three top levels (21) and 20 of the fourth, 5.1 KB).  With the 16-KB stack and the 10-KB
+// triangle batches (below) a workgroup takes 31.6 KB, so a CU still holds the 5 workgroups its
+// VGPRs allow.  Sweeps: 85 nodes without the batches and 21 / 41 / 85 before them were within
+// ±1 %; with them 41 beats 21 by 0.9 % and 5 loses 1 %.
 #ifndef PT_LDS_NODES
-#define PT_LDS_NODES 85
+#define PT_LDS_NODES 41
 #endif
 constexpr int kLdsNodes = PT_LDS_NODES;
+// wave-batched triangle tests (pt_device.h wave_tri_batch): 2.5 KB of LDS per wave
+constexpr int kTriBatchWaves = kBlockWF / 64;
+// Trace kernels: 5 waves per SIMD (96 VGPRs, no spills); the textured variants spill a few
+// VGPRs at 96 and keep 4.
 #ifndef PT_WF_WAVES
-#define PT_WF_WAVES 1
+#define PT_WF_WAVES 5
 #endif
+constexpr int wf_waves(bool tex) { return tex ? 4 : PT_WF_WAVES; }
 constexpr int kMissTri = -1;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -180,11 +188,13 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
 // This wave's static slice of a queue of length n (grid sized to residency, so every wave
 // is resident and slices balance statistically; no fetch atomics).
 #ifndef PT_REFILL_MIN
-#define PT_REFILL_MIN 24  // idle lanes before a wave refills (sweep 8 -> 24: +6.5 %)
+#define PT_REFILL_MIN 16  // idle lanes before a wave refills (24 before the triangle batches;
+                          // with them 12 / 16 / 20 / 32: -1 / 0 / -0 / -5 %)
 #endif
 constexpr int kRefillMin = PT_REFILL_MIN;
 #ifndef PT_TRI_BATCH
-#define PT_TRI_BATCH 16  // lanes with a pending leaf before a wave runs its triangle tests
+#define PT_TRI_BATCH 20  // lanes with a pending leaf before a wave runs its triangle batch (8 / 12 / 16 /
+                         // 20 / 24 / 32: -7 / -2 / -0.3 / 0 / -0.3 / -5 %)
 #endif
 
 __device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
@@ -217,7 +227,7 @@ __device__ __forceinline__ void stqs(float4* p, float4 v) {
 // slice.  Closest-hit lanes trace in [0, tmax_closest].
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
 __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, float tmax_closest, int* stk,
-                                            TravStats& ts, Fetch fetch, Finish finish) {
+                                            TriBatchLds* tri_lds, TravStats& ts, Fetch fetch, Finish finish) {
     int spill[kSpillDepth];
     TravState st;
     int ri = -1;
@@ -258,8 +268,8 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
             if (!__ballot(ri >= 0)) break;
             continue;  // only parked lanes left: the next batch block finishes them
         }
-        // postponed leaves: run the triangle half of the step once enough lanes hold a leaf,
-        // or when too few lanes have a node left to visit (then the leaves are the work)
+        // postponed leaves: test the pending leaves once enough lanes hold one, or when too few
+        // lanes have a node left to visit (then the leaves are the work)
         const int n_act = __popcll(act);
         const int n_leaf = __popcll(__ballot(active && st.leaf != kEmptyChild));
         const int n_node = __popcll(__ballot(active && st.cur >= 0));
@@ -270,16 +280,22 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
             ts.node_steps += n_node > 0;
             ts.tri_steps += tri_ok && n_leaf > 0;
         }
-        if (active && trav_step<ANY, STATS, kStack, TEX>(S, st, stk, kBlockWF, spill, ts, tri_ok)) done = true;
+        // the triangles of every pending leaf in one wave batch (pt_device.h wave_tri_batch),
+        // then the node half of the step
+        if (tri_ok && n_leaf > 0) {  // wave-uniform
+            wave_tri_batch<ANY, STATS, TEX>(S, st, active && st.leaf != kEmptyChild, tri_lds, ts);
+            if (active && is_any<ANY>(st) && st.h.tri >= 0) done = true;
+        }
+        if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockWF, spill, ts)) done = true;
     }
 }
 
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
-__device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TravStats& ts, Fetch fetch,
-                                            Finish finish) {
+__device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, TriBatchLds* tri_lds, TravStats& ts,
+                                            Fetch fetch, Finish finish) {
     int next, end;
     wave_slice(n, next, end);
-    trace_range<ANY, STATS, TEX>(S, next, end, 100.0f, stk, ts, fetch, finish);
+    trace_range<ANY, STATS, TEX>(S, next, end, 100.0f, stk, tri_lds, ts, fetch, finish);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -288,10 +304,12 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
 // and each hit record is written to all copies.  The records are bit-identical to tracing every
 // copy; DESIGN.md §5 gives the A/B.
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WFState W, int b, int dup,
+__global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_extend(DevScene S, WFState W, int b, int dup,
                                                                   unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    __shared__ TriBatchLds tri_batch[kTriBatchWaves];
+    TriBatchLds* tri_lds = tri_batch + (threadIdx.x >> 6);
     stage_top_nodes<kLdsNodes>(S, top);
     const int n = *cnt(W, b, kQueue);
     const int n_trace = n / dup;
@@ -300,7 +318,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_extend(DevScene S, WF
     int* stk = stack + threadIdx.x;
     TravStats ts;
     trace_slice<kRayClosest, STATS, TEX>(
-        S, n_trace, stk, ts,
+        S, n_trace, stk, tri_lds, ts,
         [&](int ri, TravState& st) {
             const float4 a = ro[ri], c = rd[ri];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
@@ -478,10 +496,12 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
 // and one launch instead of two).  Items [0, n_ext) are extension rays (closest hit ->
 // hit records), items [n_ext, n_ext + n_sh) shadow rays (any hit -> deferred NEE add).
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S, WFState W, int b,
+__global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    __shared__ TriBatchLds tri_batch[kTriBatchWaves];
+    TriBatchLds* tri_lds = tri_batch + (threadIdx.x >> 6);
     stage_top_nodes<kLdsNodes>(S, top);
     const int n_ext = *cnt(W, b + 1, kQueue);
     const int n_sh = *cnt(W, b, kShadowQ);
@@ -523,7 +543,7 @@ __global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_trace_pair(DevScene S
     // per-wave shares of both kinds were slower).
     int first, end;
     wave_slice(n_ext + n_sh, first, end);
-    trace_range<kRayMixed, STATS, TEX>(S, first, end, 100.0f, stk, ts, fetch, finish);
+    trace_range<kRayMixed, STATS, TEX>(S, first, end, 100.0f, stk, tri_lds, ts, fetch, finish);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
@@ -585,17 +605,19 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
 }
 
 template <bool TEX>
-__global__ __launch_bounds__(kBlockWF, PT_WF_WAVES) void k_shadow_vis(DevScene S, WFState W, int b,
+__global__ __launch_bounds__(kBlockWF, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    __shared__ TriBatchLds tri_batch[kTriBatchWaves];
+    TriBatchLds* tri_lds = tri_batch + (threadIdx.x >> 6);
     stage_top_nodes<kLdsNodes>(S, top);
     const int n = *cnt(W, b, kShadowQ);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[5], (unsigned long long)n);
     int* stk = stack + threadIdx.x;
     TravStats ts;
     trace_slice<kRayAny, false, TEX>(
-        S, n, stk, ts,
+        S, n, stk, tri_lds, ts,
         [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
