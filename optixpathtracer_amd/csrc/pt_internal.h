@@ -47,8 +47,10 @@ struct WFState {
     float4* sh_d = nullptr;                 // direction | tmax
     float4* sh_c = nullptr;                 // deferred NEE contribution (fused modes)
     int* aux = nullptr;                     // light index << 1 | conductor (RNG-coupled modes)
-    int* vis = nullptr;                     // shadow result per path (RNG-coupled modes)
-    int* count = nullptr;                   // [2b] queue length of bounce b, [2b+1] shadow count
+    int* vis = nullptr;                     // shadow result per shadow ray (RNG-coupled modes)
+    int* nq = nullptr;                      // NEE items (RNG-coupled modes): kShadeBuckets regions of `paths`
+    int* sq = nullptr;                      // BSDF-sample items, same layout
+    int* count = nullptr;                   // per bounce: queue, shadow, NEE and sample bucket lengths
     int paths = 0;
     int max_bounces = 0;
 };

@@ -19,9 +19,11 @@
 //                         (closest hit), which start at the same hit points
 //     RNG-coupled modes (Default / Layered: GlossyDiffuse::f consumes the path seed only
 //     when the light is visible, GlossyDiffuse.h:230-343):
-//       k_shade_a       : surface, coin, light pick -> shadow ray queue
-//       k_shadow_vis    : any-hit -> vis[path]
-//       k_shade_b       : if visible: f (may draw), NEE; BSDF sample -> queue b+1
+//       k_shade_a       : surface, coin, light pick -> shadow ray queue; item -> bucketed
+//                         sample queue (and NEE queue at bounce 0, from the visibility table)
+//       k_shadow_vis    : any-hit -> vis[shadow ray]; k_nee_compact: visible -> NEE queue
+//       k_shade_nee     : f (may draw), NEE, over the bucketed NEE queue
+//       k_shade_smp     : BSDF sample -> queue b+1, over the bucketed sample queue
 //   k_accum             : accum[pixel] += L[f * P + pixel] for f = 0 .. nf-1 in order (the same
 //                         fp32 order as the sequential reference accumulation)
 //
@@ -101,9 +103,12 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
 
 // Per-bounce counters: queue length and shadow-queue length, each on its own 128-B line
 // (appends from different queues never contend for one L2 line).  Zeroed per frame.
-constexpr int kCnt = 2;
+// Default / Layered shading items are queued per bucket (shade_bucket): kShadeBuckets NEE and
+// kShadeBuckets BSDF-sample counters follow the two queue counters.
+constexpr int kShadeBuckets = 3;
+constexpr int kCnt = 2 + 2 * kShadeBuckets;
 constexpr int kCntStride = 32;  // ints per counter = 128 B
-enum { kQueue = 0, kShadowQ = 1 };
+enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kShadeBuckets };
 __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
 inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * kCnt * (size_t)(max_bounces + 2); }
 
@@ -128,13 +133,10 @@ constexpr int kWavesSh = kBlockSh / 64;
 #define PT_SHF_WAVES_OTHER 1
 #endif
 constexpr int shf_waves(int mode) { return (mode == 1 || mode == 3) /*Lambert, Dielectric*/ ? PT_SHF_WAVES : PT_SHF_WAVES_OTHER; }
-// k_shade_b (Default / Layered: the stochastic GlossyDiffuse eval + sample) runs in 256-thread
-// blocks at 4 waves per SIMD (128 VGPRs).  Its two phases are separated by a block barrier, and
-// a 1024-thread block (one per CU) held every SIMD slot of the CU while the waves without NEE
-// items waited at it; four independent 256-thread blocks per CU fill those slots with other
-// blocks' work: Layered 375 -> 433, Default 366 -> 408, Sponza-class 245 -> 258 Msamples/s
-// (1024 / 512 / 128 / 64 threads: 375 / 431 / 427 / 425 Layered; 168 VGPRs at 3 waves per SIMD:
-// 402).
+// k_shade_nee / k_shade_smp (Default / Layered: the stochastic GlossyDiffuse eval, the sample)
+// run in 256-thread blocks at 4 waves per SIMD (128 VGPRs).  (Round 2 before the bucketed
+// queues: one kernel with both phases behind a block barrier, where 256-thread blocks beat
+// 1024 / 512 / 128 / 64 threads: Layered 433 vs 375 / 431 / 427 / 425 Msamples/s)
 #ifndef PT_SHB_BLOCK
 #define PT_SHB_BLOCK 256
 #endif
@@ -165,6 +167,48 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     __syncthreads();
     return lds[WAVES] + lds[wave] + prefix;
 }
+
+// Block-wide append into K bucket regions (counter of bucket k at counter0 + k * kCntStride):
+// threads with bucket k in [0, K) get consecutive slots of region k in thread order, bucket < 0
+// appends nothing.  One atomic per non-empty bucket per block.  `lds` holds K * (WAVES + 1) ints.
+template <int WAVES, int K>
+__device__ __forceinline__ int block_append_k(int* counter0, int bucket, int* lds) {
+    const int wave = threadIdx.x >> 6;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const unsigned long long m = __ballot(bucket == k ? 1 : 0);
+        if (bucket == k) mine = m;
+        if (lane_id() == 0) lds[k * WAVES + wave] = __popcll(m);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < K) {
+        const int k = threadIdx.x;
+        int tot = 0;
+        for (int w = 0; w < WAVES; ++w) {
+            const int c = lds[k * WAVES + w];
+            lds[k * WAVES + w] = tot;
+            tot += c;
+        }
+        lds[K * WAVES + k] = tot > 0 ? atomicAdd(counter0 + k * kCntStride, tot) : 0;
+    }
+    __syncthreads();
+    if (bucket < 0) return 0;
+    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    return lds[K * WAVES + bucket] + lds[bucket * WAVES + wave] + pre;
+}
+
+// Bucket of a Default / Layered shading item.  The items of one bucket run the same BSDF code
+// path, so the NEE and sample kernels take them from per-bucket queue regions and their waves
+// hold one kind of item: 0 = conductor (Default mode's metallic coin, devicePrograms.cu:400),
+// 1 / 2 = the layered BSDF with a smooth / rough top interface (layered_f's topSpec: alpha =
+// roughness^2 < 1e-3, GlossyDiffuse.h).
+template <int MODE>
+__device__ __forceinline__ int shade_bucket(bool conductor, float roughness) {
+    if (MODE == kModeDefault && conductor) return 0;
+    return sqr(roughness) < 1e-3f ? 1 : 2;
+}
+constexpr int kItemBits = 28;  // a queue item index is < 2^28 (kMaxWFPaths); the bucket sits above it
 
 // Paths of nf consecutive frames are in flight together (path q = f * P + pixel), so every
 // launch works on nf frames' queues: fewer launches and one SIMT tail per nf frames.
@@ -553,59 +597,77 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
     flush_trav_stats<STATS>(counters, ts);
 }
 
+// First half of a Default / Layered bounce: surface, metallic coin and light pick (the draws
+// GlossyDiffuse::f must follow, devicePrograms.cu:400-445), then the item is queued for the
+// later phases, by bucket (shade_bucket): the BSDF-sample queue for every hit that continues,
+// and either a shadow ray (visibility still unknown; the ray carries item | bucket << 28) or,
+// at bounce 0 with the (pixel, light) visibility table, the NEE queue directly.
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
     __shared__ int lds_sh[kWavesSh + 1];
+    __shared__ int lds_nee[kShadeBuckets * (kWavesSh + 1)], lds_smp[kShadeBuckets * (kWavesSh + 1)];
     if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
-    {
-        const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
-        const bool valid = i < n;
-        bool emit = false;
-        f3 so, sdir;
-        float stmax = 0.0f;
-        int path = 0;
-        if (valid) {
-            const float4 hv = W.hit[i];
-            path = __float_as_int(hv.x);
-            const Hit h = decode_hit(hv);
-            if (h.tri >= 0) {
-                const float4 c = rd[i];
-                SurfaceHit sf;
-                reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
-                float4 bv = W.beta[path];
-                uint32_t seed = __float_as_uint(bv.w);
-                if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
-                    const float4 l = W.L[path];
-                    debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, mk(bv.x, bv.y, bv.z),
-                                 mk(l.x, l.y, l.z));
-                }
-                const bool conductor = rnd(seed) < sf.metallic;
-                int li;
-                const float P = pick_light(L, seed, li);
-                W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));
-                W.aux[path] = (li << 1) | (conductor ? 1 : 0);
-                if (P > 0.0f && !vis0) {
+    const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+    bool emit = false;
+    int nee_bucket = -1, smp_bucket = -1, code = 0;
+    f3 so, sdir;
+    float stmax = 0.0f;
+    if (i < n) {
+        const float4 hv = W.hit[i];
+        const int path = __float_as_int(hv.x);
+        const Hit h = decode_hit(hv);
+        if (h.tri >= 0) {
+            const float4 c = rd[i];
+            SurfaceHit sf;
+            reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
+            float4 bv = W.beta[path];
+            uint32_t seed = __float_as_uint(bv.w);
+            if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
+                const float4 l = W.L[path];
+                debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, mk(bv.x, bv.y, bv.z),
+                             mk(l.x, l.y, l.z));
+            }
+            const bool conductor = rnd(seed) < sf.metallic;
+            int li;
+            const float P = pick_light(L, seed, li);
+            W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));
+            W.aux[path] = (li << 1) | (conductor ? 1 : 0);
+            const int bk = shade_bucket<MODE>(conductor, sf.roughness);
+            // the last bounce's sampled direction is never traced (SamplePath :646): no sample item
+            if (b + 1 < L.max_bounces) smp_bucket = bk;
+            if (P > 0.0f) {
+                if (vis0) {
+                    if (W.vis[vis0_index(L, path, li)]) nee_bucket = bk;
+                } else {
                     const DevLight lt = L.lights[li];
                     f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
                     so = sf.pos + 1e-3f * sf.ng;
                     sdir = normalize(ldir);
                     stmax = length(ldir);
+                    code = i | (bk << kItemBits);
                     emit = true;
                 }
             }
         }
-        const int si = block_append(cnt(W, b, kShadowQ), emit, lds_sh);
-        if (emit) {
-            W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(path));
-            W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
-        }
     }
+    const int si = block_append(cnt(W, b, kShadowQ), emit, lds_sh);
+    if (emit) {
+        W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(code));
+        W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
+    }
+    const int ni = block_append_k<kWavesSh, kShadeBuckets>(cnt(W, b, kNee0), nee_bucket, lds_nee);
+    if (nee_bucket >= 0) W.nq[(size_t)nee_bucket * W.paths + ni] = i;
+    const int mi = block_append_k<kWavesSh, kShadeBuckets>(cnt(W, b, kSmp0), smp_bucket, lds_smp);
+    if (smp_bucket >= 0) W.sq[(size_t)smp_bucket * W.paths + mi] = i;
 }
 
+// Any-hit visibility of the shadow queue of bounce b.  table = 1: the bounce-0 (pixel, light)
+// table (k_shadow0_setup), vis[j] = 1 if unoccluded; table = 0: vis[j] = the ray's item code
+// if unoccluded, else -1 (k_nee_compact reads it).
 template <bool TEX>
-__global__ __launch_bounds__(kBlockWF, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b,
+__global__ __launch_bounds__(kBlockWF, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b, int table,
                                                                       unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
@@ -621,112 +683,140 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(false)) void k_shadow_vis(DevSce
         [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
+            st.path = __float_as_int(a.w);
         },
-        [&](int j, const TravState& st) { W.vis[__float_as_int(W.sh_o[j].w)] = st.h.tri >= 0 ? 0 : 1; });
+        [&](int j, const TravState& st) {
+            const bool occluded = st.h.tri >= 0;
+            W.vis[j] = table ? (occluded ? 0 : 1) : (occluded ? -1 : st.path);
+        });
 }
 
-// Block-local stable two-bucket compaction: threads with `pred` get consecutive slots, those
-// with bucket 0 first; returns the slot (valid if pred) and the block's total.
-template <int WAVES>
-__device__ __forceinline__ int block_bucket_scan(bool pred, bool bucket1, int* lds, int& total) {
-    const unsigned long long m0 = __ballot(pred && !bucket1 ? 1 : 0);
-    const unsigned long long m1 = __ballot(pred && bucket1 ? 1 : 0);
-    const int wave = threadIdx.x >> 6;
-    if (lane_id() == 0) {
-        lds[wave] = __popcll(m0);
-        lds[WAVES + wave] = __popcll(m1);
+// Visible shadow rays of bounce b -> the NEE bucket queues (vis[j] = item | bucket << 28, or -1).
+// kCompactPer consecutive entries per thread, so a block appends 8192 entries with one atomic
+// per bucket.
+constexpr int kCompactPer = 8;
+__global__ __launch_bounds__(kBlockSh) void k_nee_compact(WFState W, int b) {
+    const int n = *cnt(W, b, kShadowQ);
+    const int base = (int)(blockIdx.x * kBlockSh * kCompactPer);
+    if (base >= n) return;  // block-uniform
+    __shared__ int lds[kShadeBuckets * (kWavesSh + 1)];
+    const int j0 = base + (int)threadIdx.x * kCompactPer;
+    int v[kCompactPer];
+    int c[kShadeBuckets] = {};
+#pragma unroll
+    for (int k = 0; k < kCompactPer; ++k) {
+        v[k] = j0 + k < n ? W.vis[j0 + k] : -1;
+#pragma unroll
+        for (int q = 0; q < kShadeBuckets; ++q) c[q] += (v[k] >= 0 && (v[k] >> kItemBits) == q) ? 1 : 0;
+    }
+    // block-exclusive prefix of every bucket's count: wave scan, then the wave totals in LDS
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    int incl[kShadeBuckets];
+#pragma unroll
+    for (int q = 0; q < kShadeBuckets; ++q) {
+        int x = c[q];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        incl[q] = x;
+        if (lane == 63) lds[q * kWavesSh + wave] = x;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if ((int)threadIdx.x < kShadeBuckets) {
+        const int q = threadIdx.x;
         int tot = 0;
-        for (int w = 0; w < 2 * WAVES; ++w) {  // bucket 0 of every wave, then bucket 1
-            const int c = lds[w];
-            lds[w] = tot;
-            tot += c;
+        for (int w = 0; w < kWavesSh; ++w) {
+            const int t = lds[q * kWavesSh + w];
+            lds[q * kWavesSh + w] = tot;
+            tot += t;
         }
-        lds[2 * WAVES] = tot;
+        lds[kShadeBuckets * kWavesSh + q] = tot > 0 ? atomicAdd(cnt(W, b, kNee0 + q), tot) : 0;
     }
     __syncthreads();
-    total = lds[2 * WAVES];
-    const unsigned long long m = bucket1 ? m1 : m0;
-    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    return lds[(bucket1 ? WAVES : 0) + wave] + pre;
+    int off[kShadeBuckets];
+#pragma unroll
+    for (int q = 0; q < kShadeBuckets; ++q)
+        off[q] = lds[kShadeBuckets * kWavesSh + q] + lds[q * kWavesSh + wave] + incl[q] - c[q];
+#pragma unroll
+    for (int k = 0; k < kCompactPer; ++k) {
+        if (v[k] < 0) continue;
+        const int q = v[k] >> kItemBits;
+        int slot = off[0];
+#pragma unroll
+        for (int r = 1; r < kShadeBuckets; ++r) slot = q == r ? off[r] : slot;
+#pragma unroll
+        for (int r = 0; r < kShadeBuckets; ++r) off[r] += q == r ? 1 : 0;
+        W.nq[(size_t)q * W.paths + slot] = v[k] & ((1 << kItemBits) - 1);
+    }
 }
 
-// Second half of a Default / Layered bounce.  The stochastic GlossyDiffuse eval and sample
-// dominate (≈10^4 instructions per call) and a wave pays for its slowest lane,
-// so the block first compacts its items in LDS: the NEE eval runs on the items whose light is
-// visible, packed into the block's first waves and grouped by material (conductor coin), then
-// the BSDF sample runs on the items that hit a surface, packed and grouped the same way.
-// Every path still sees the same operations and random numbers in the same order (the NEE
-// eval updates the path seed in W.beta before the sample reads it); only which thread works
-// on which path, and the order of the appends to the next queue, change.
+// Entry idx of a bucketed queue (region k: q[k * paths ...], length *cnt(W, b, c0 + k)), or -1
+// past the total.  Regions are taken in bucket order, so all but two waves hold one bucket.
+__device__ __forceinline__ int bucket_entry(const WFState& W, const int* q, int b, int c0, int idx) {
+    const int n0 = *cnt(W, b, c0), n1 = *cnt(W, b, c0 + 1), n2 = *cnt(W, b, c0 + 2);
+    static_assert(kShadeBuckets == 3, "bucket_entry walks three regions");
+    if (idx < n0) return q[idx];
+    if (idx < n0 + n1) return q[(size_t)W.paths + (idx - n0)];
+    if (idx < n0 + n1 + n2) return q[2 * (size_t)W.paths + (idx - n0 - n1)];
+    return -1;
+}
+__device__ __forceinline__ int bucket_total(const WFState& W, int b, int c0) {
+    return *cnt(W, b, c0) + *cnt(W, b, c0 + 1) + *cnt(W, b, c0 + 2);
+}
+
+// NEE of a Default / Layered bounce over the items whose light is visible (devicePrograms.cu:
+// 446-472).  The stochastic GlossyDiffuse eval dominates (≈10^4 instructions per call, DESIGN.md
+// §5) and a wave pays for its slowest lane: the items come from the bucketed NEE queue, so every
+// wave but the last of each bucket is full and runs one BSDF code path.  Every path sees the
+// same operations and random numbers in the same order (the eval writes the advanced seed back
+// to W.beta before k_shade_smp reads it).
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_b(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+__global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene S, DevLaunch L, WFState W, int b) {
+    if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kNee0)) return;  // block-uniform
+    const int j = bucket_entry(W, W.nq, b, kNee0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
+    if (j < 0) return;  // no barrier below
+    const float4 hv = W.hit[j], c = W.ray_d[b & 1][j];
+    const int path = __float_as_int(hv.x);
+    const Hit h = decode_hit(hv);
+    SurfaceHit sf;
+    reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
+    const float4 bv = W.beta[path];
+    uint32_t seed = __float_as_uint(bv.w);
+    const f3 beta = mk(bv.x, bv.y, bv.z);
+    const int aux = W.aux[path];
+    const int li = aux >> 1;
+    const float P = L.n_lights == 1 ? 1.0f : 1.0f / (float)L.n_lights;
+    const DevLight lt = L.lights[li];
+    f3 lpos = mk(lt.px, lt.py, lt.pz);
+    f3 lds = to_local(sf.fr, normalize(lpos - sf.pos));
+    f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
+    f3 spectrum = f * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+    if (!is_zero(spectrum)) {
+        f3 dd = sf.pos - lpos;
+        float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+        f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+        f3 add = ((beta * spectrum) * Li) / (P * 1.0f);
+        float4 l = W.L[path];
+        W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
+    }
+    W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));  // f may draw
+}
+
+// BSDF sample + continuation of a Default / Layered bounce (devicePrograms.cu:474-509) over the
+// bucketed sample queue; continuation rays are appended to queue b + 1.
+template <int MODE, bool TEX>
+__global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_smp(DevScene S, DevLaunch L, WFState W, int b) {
     constexpr int kW = kBlockShB / 64;
-    const int n = *cnt(W, b, kQueue);
-    const float4* rd = W.ray_d[b & 1];
-    float4* no = W.ray_o[(b + 1) & 1];
-    float4* nd = W.ray_d[(b + 1) & 1];
     __shared__ int lds_q[kW + 1];
-    __shared__ int lds_scan_a[2 * kW + 1], lds_scan_b[2 * kW + 1];  // separate: no reuse race
-    __shared__ int lds_nee[kBlockShB], lds_smp[kBlockShB];
-    if ((int)(blockIdx.x * kBlockShB) >= n) return;  // block-uniform
-    const int i = (int)(blockIdx.x * kBlockShB + threadIdx.x);
-    bool hit = false, nee = false, conductor = false;
-    if (i < n) {
-        const float4 hv = W.hit[i];
-        const int path = __float_as_int(hv.x);
-        hit = __float_as_int(hv.w) != kMissTri;
-        if (hit) {
-            const int aux = W.aux[path];
-            conductor = aux & 1;
-            nee = L.n_lights > 0 && W.vis[vis0 ? vis0_index(L, path, aux >> 1) : path];
-        }
-    }
-    int n_nee, n_smp;
-    const int s_nee = block_bucket_scan<kW>(nee, conductor, lds_scan_a, n_nee);
-    if (nee) lds_nee[s_nee] = i;
-    // the last bounce's sampled direction is never traced (SamplePath :646): no sample items
-    const bool smp = hit && b + 1 < L.max_bounces;
-    const int s_smp = block_bucket_scan<kW>(smp, conductor, lds_scan_b, n_smp);
-    if (smp) lds_smp[s_smp] = i;
-    __syncthreads();
-    if ((int)threadIdx.x < n_nee) {  // NEE: the light is visible (devicePrograms.cu:446-472)
-        const int j = lds_nee[threadIdx.x];
-        const float4 hv = W.hit[j], c = rd[j];
-        const int path = __float_as_int(hv.x);
-        const Hit h = decode_hit(hv);
-        SurfaceHit sf;
-        reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
-        const float4 bv = W.beta[path];
-        uint32_t seed = __float_as_uint(bv.w);
-        const f3 beta = mk(bv.x, bv.y, bv.z);
-        const int aux = W.aux[path];
-        const int li = aux >> 1;
-        const float P = L.n_lights == 1 ? 1.0f : 1.0f / (float)L.n_lights;
-        const DevLight lt = L.lights[li];
-        f3 lpos = mk(lt.px, lt.py, lt.pz);
-        f3 lds = to_local(sf.fr, normalize(lpos - sf.pos));
-        f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
-        f3 spectrum = f * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
-        if (!is_zero(spectrum)) {
-            f3 dd = sf.pos - lpos;
-            float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
-            f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
-            f3 add = ((beta * spectrum) * Li) / (P * 1.0f);
-            float4 l = W.L[path];
-            W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
-        }
-        W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));  // f may draw
-    }
-    __syncthreads();  // the sample below reads the seeds written above (same block)
+    if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kSmp0)) return;  // block-uniform
+    const int j = bucket_entry(W, W.sq, b, kSmp0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
     bool emit_next = false;
     f3 o, d;
     int path = 0;
-    if ((int)threadIdx.x < n_smp) {  // BSDF sample + continuation (devicePrograms.cu:474-509)
-        const int j = lds_smp[threadIdx.x];
-        const float4 hv = W.hit[j], c = rd[j];
+    if (j >= 0) {
+        const float4 hv = W.hit[j], c = W.ray_d[b & 1][j];
         path = __float_as_int(hv.x);
         const Hit h = decode_hit(hv);
         d = mk(c.x, c.y, c.z);
@@ -741,6 +831,8 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_b(DevScene S,
             W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
         }
     }
+    float4* no = W.ray_o[(b + 1) & 1];
+    float4* nd = W.ray_d[(b + 1) & 1];
     const int qi = block_append<kW>(cnt(W, b + 1, kQueue), emit_next, lds_q);
     if (emit_next) {
         no[qi] = make_float4(o.x, o.y, o.z, __int_as_float(path));
@@ -809,6 +901,7 @@ dim3 occupancy_grid(K kernel, int cus) {
     return dim3((unsigned)(per_cu * std::max(1, cus)));
 }
 
+// phase (Default / Layered): 0 = k_shade_a, 1 = k_shade_nee, 2 = k_shade_smp
 template <int MODE, bool TEX>
 hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
                           hipStream_t stream, int phase, int vis0) {
@@ -819,9 +912,12 @@ hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, con
     } else if (phase == 0) {
         hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b,
                            vis0);
+    } else if (phase == 1) {
+        hipLaunchKernelGGL((k_shade_nee<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L,
+                           W, b);
     } else {
-        hipLaunchKernelGGL((k_shade_b<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L, W,
-                           b, vis0);
+        hipLaunchKernelGGL((k_shade_smp<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L,
+                           W, b);
     }
     return hipGetLastError();
 }
@@ -856,7 +952,7 @@ hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStre
 size_t wavefront_bytes(int paths, int max_bounces) {
     size_t P = (size_t)paths;
     return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 2 /*beta, L*/ + 3 /*shadow*/) +
-           P * 2 * sizeof(int) + count_bytes(max_bounces);
+           P * (2 + 2 * kShadeBuckets) * sizeof(int) + count_bytes(max_bounces);
 }
 
 hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
@@ -877,6 +973,8 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
     al((void**)&W.sh_c, P * sizeof(float4));
     al((void**)&W.aux, P * sizeof(int));
     al((void**)&W.vis, P * sizeof(int));
+    al((void**)&W.nq, P * kShadeBuckets * sizeof(int));
+    al((void**)&W.sq, P * kShadeBuckets * sizeof(int));
     al((void**)&W.count, count_bytes(max_bounces));
     W.paths = paths;
     W.max_bounces = max_bounces;
@@ -885,7 +983,7 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
 
 void wavefront_free(WFState& W) {
     void* ps[] = {W.ray_o[0], W.ray_o[1], W.ray_d[0], W.ray_d[1], W.hit, W.beta, W.L, W.sh_o, W.sh_d, W.sh_c,
-                  W.aux, W.vis, W.count};
+                  W.aux, W.vis, W.nq, W.sq, W.count};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     W = WFState{};
@@ -945,13 +1043,14 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         ++timed;
         return hipGetLastError();
     };
-    auto shadow_vis = [&](int b) -> hipError_t {
+    auto shadow_vis = [&](int b, int table) -> hipError_t {
         if (tex)
             hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0, stream,
-                               S, W, b, L.counters);
+                               S, W, b, table, L.counters);
         else
             hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockWF), 0,
-                               stream, S, W, b, L.counters);
+                               stream, S, W, b, table, L.counters);
+        if (!table) hipLaunchKernelGGL(k_nee_compact, item_grid(P, kBlockSh * kCompactPer), dim3(kBlockSh), 0, stream, W, b);
         return hipGetLastError();
     };
     // bounce-0 shadow dedup: one shadow ray per (pixel, light) instead of one per path; pays
@@ -967,7 +1066,7 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
             hipLaunchKernelGGL(k_shadow0_setup<false>, item_grid(P1 * vis0, kBlockWF), dim3(kBlockWF), 0, stream, S,
                                L, W);
         hipError_t r = hipGetLastError();
-        if (r != hipSuccess || (r = shadow_vis(0)) != hipSuccess) return r;
+        if (r != hipSuccess || (r = shadow_vis(0, 1)) != hipSuccess) return r;
         // the table's rays must not be traced again as bounce-0 shadow rays
         return hipMemsetAsync(W.count + kShadowQ * kCntStride, 0, sizeof(int), stream);
     };
@@ -987,9 +1086,13 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
             if ((e = extend(b, b == 0 && primary_dedup ? nf : 1)) != hipSuccess) return e;
             const int v0 = b == 0 ? vis0 : 0;
             if (v0 && (e = shadow0()) != hipSuccess) return e;
+            // k_shade_a queues the bounce's items by bucket; the visible ones (the bounce-0 table,
+            // or k_shadow_vis + k_nee_compact) get the NEE eval, the continuing ones the sample
             if ((e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 0, v0)) != hipSuccess) return e;
-            if (!v0 && (e = shadow_vis(b)) != hipSuccess) return e;
+            if (!v0 && (e = shadow_vis(b, 0)) != hipSuccess) return e;
             if ((e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 1, v0)) != hipSuccess) return e;
+            if (b + 1 < maxb && (e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 2, v0)) != hipSuccess)
+                return e;
         }
     }
     hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
