@@ -41,7 +41,9 @@ struct WFState {
     float4* ray_o[2] = {nullptr, nullptr};  // queue b&1: origin.xyz | path id
     float4* ray_d[2] = {nullptr, nullptr};  // direction.xyz | 0
     float4* hit = nullptr;                  // path, u, v, tri | back<<31 (-1 = miss), queue order
-    float4* beta = nullptr;                 // path throughput.xyz | seed, path order
+    float4* beta = nullptr;                 // path throughput.xyz | seed: path order (Default / Layered),
+                                            // queue order of the even bounces (fused modes)
+    float4* beta_q = nullptr;               // fused modes: throughput | seed of the odd bounces' queues
     float4* L = nullptr;                    // path radiance of the frame, path order
     float4* sh_o = nullptr;                 // shadow queue: origin | path
     float4* sh_d = nullptr;                 // direction | tmax

@@ -110,6 +110,12 @@ constexpr int kCnt = 2 + 2 * kShadeBuckets;
 constexpr int kCntStride = 32;  // ints per counter = 128 B
 enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kShadeBuckets };
 __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
+// Path throughput | seed.  W.beta in path order (the phases of a bounce read it by path), except
+// in the Lambert mode: in queue order next to the ray, ping-pong like ray_o / ray_d (queue b
+// in W.beta for even b, W.beta_q for odd b), so k_shade_fused streams it instead of gathering it
+// by path: a random 16-B read costs a 64-B line fetch (DESIGN.md §4 counter calibration).
+// Queue 0 is in path order, so k_camera's W.beta[q] serves both layouts.
+__device__ __forceinline__ float4* queue_beta(const WFState& W, int b) { return (b & 1) ? W.beta_q : W.beta; }
 inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * kCnt * (size_t)(max_bounces + 2); }
 
 // Shading kernels: 1024-thread blocks, one queue item per thread over a grid sized to the
@@ -453,6 +459,10 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
 
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+    // Lambert (memory-bound, 56 VGPRs): the throughput in queue order (queue_beta), +1.6 %; the
+    // Conductor and Dielectric kernels are register-bound, and holding it across the appends
+    // cost them 1-2 %, so they gather it by path
+    constexpr bool kBetaQ = MODE == kModeLambert;
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
@@ -463,7 +473,8 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
         const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
         const bool valid = i < n;
         bool emit_shadow = false, emit_next = false;
-        f3 so, sdir, contrib, o, d;
+        f3 so, sdir, contrib, o, d, beta;
+        uint32_t seed = 0;
         float stmax = 0.0f;
         int path = 0;
         if (valid) {
@@ -475,9 +486,9 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
-                float4 bv = ldqs(W.beta + path);
-                uint32_t seed = __float_as_uint(bv.w);
-                f3 beta = mk(bv.x, bv.y, bv.z);
+                float4 bv = ldqs(kBetaQ ? queue_beta(W, b) + i : W.beta + path);
+                seed = __float_as_uint(bv.w);
+                beta = mk(bv.x, bv.y, bv.z);
                 if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
                     const float4 l = W.L[path];
                     debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, beta, mk(l.x, l.y, l.z));
@@ -517,7 +528,7 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 if (b + 1 < L.max_bounces &&
                     bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
                     emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
-                    stqs(W.beta + path, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
+                    if (!kBetaQ) stqs(W.beta + path, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
                 }
             }
         }
@@ -531,6 +542,7 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
+            if (kBetaQ) stqs(queue_beta(W, b + 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
         }
     }
 }
@@ -951,7 +963,7 @@ hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStre
 
 size_t wavefront_bytes(int paths, int max_bounces) {
     size_t P = (size_t)paths;
-    return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 2 /*beta, L*/ + 3 /*shadow*/) +
+    return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 3 /*beta x2, L*/ + 3 /*shadow*/) +
            P * (2 + 2 * kShadeBuckets) * sizeof(int) + count_bytes(max_bounces);
 }
 
@@ -967,6 +979,7 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
     al((void**)&W.ray_d[1], P * sizeof(float4));
     al((void**)&W.hit, P * sizeof(float4));
     al((void**)&W.beta, P * sizeof(float4));
+    al((void**)&W.beta_q, P * sizeof(float4));
     al((void**)&W.L, P * sizeof(float4));
     al((void**)&W.sh_o, P * sizeof(float4));
     al((void**)&W.sh_d, P * sizeof(float4));
@@ -982,7 +995,7 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
 }
 
 void wavefront_free(WFState& W) {
-    void* ps[] = {W.ray_o[0], W.ray_o[1], W.ray_d[0], W.ray_d[1], W.hit, W.beta, W.L, W.sh_o, W.sh_d, W.sh_c,
+    void* ps[] = {W.ray_o[0], W.ray_o[1], W.ray_d[0], W.ray_d[1], W.hit, W.beta, W.beta_q, W.L, W.sh_o, W.sh_d, W.sh_c,
                   W.aux, W.vis, W.nq, W.sq, W.count};
     for (void* p : ps)
         if (p) (void)hipFree(p);
