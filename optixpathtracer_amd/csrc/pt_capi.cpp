@@ -143,7 +143,7 @@ struct pt_renderer {
     double last_ms = 0.0, total_ms = 0.0;
     uint64_t calls = 0;
     double bvh_ms = 0.0;
-    int frames_per_launch = 64;  // 22 GB of queues at 1080p (16 -> 64 frames +5 % Lambert)
+    int frames_per_launch = 64;  // 28 GB of queues at 1080p (16 -> 64 frames +5 % Lambert)
     // multi-device (pt_options.n_devices >= 1): this renderer is device 0 of the list; peers are
     // single-device renderers of the other devices; comms[g] is device g's RCCL communicator
     std::vector<pt_renderer*> peers;
@@ -238,10 +238,10 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
     if (accum64 && kernel != PT_KERNEL_WAVEFRONT)
         return fail(PT_ERR_INVALID, "fp64 accumulation (pt_set_accum_fp64) runs with the wavefront kernel");
     if (kernel == PT_KERNEL_WAVEFRONT) {
-        // Frames per wavefront launch chain: the queues hold nf frames' paths (168 B each), at most
+        // Frames per wavefront launch chain: the queues hold nf frames' paths (208 B each), at most
         // kMaxWFPaths of them.  Batching amortises launch gaps and the per-kernel SIMT tail:
         // Lambert 1080p 545 / 648 / 664 Msamples/s at 1 / 8 / 16 frames.
-        constexpr int kMaxWFPaths = 1 << 28;  // 45 GB of queues at 168 B per path
+        constexpr int kMaxWFPaths = 1 << 28;  // 56 GB of queues at 208 B per path
         const int P = r->width * r->height;
         const int nf_cap = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
                                                  kMaxWFPaths / std::max(1, P)}));

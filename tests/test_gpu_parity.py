@@ -354,6 +354,32 @@ def test_shallow_depth_and_light_count(depth, mode, n_lights):
     assert abs(sw["segments"] - segs) <= 0.01 * segs + 2
 
 
+@pytest.mark.parametrize("n_lights", [0, 1])
+@pytest.mark.parametrize("variant,mode", [("conductor", 0), ("layered", 4), ("conductor", 4), ("diffuse", 0)])
+def test_bucketed_shading_queues(variant, mode, n_lights):
+    """Default / Layered shading runs over bucketed NEE and sample queues (k_shade_a ->
+    k_shadow_vis -> k_nee_compact -> k_shade_nee -> k_shade_smp; buckets: conductor, smooth-top
+    and rough-top layered).  No lights (no NEE items at all), one light (the bounce-0 table with
+    batching, shadow rays without), conductor and layered items mixed or alone: the images equal
+    the megakernel's (one thread per path, no queues) bit for bit, with equal segment counts."""
+    import dataclasses
+
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene(variant)
+    sc = dataclasses.replace(sc, lights=np.ascontiguousarray(sc.lights[:n_lights], np.float32).reshape(n_lights, 6))
+    mega, sm = gpu_render(sc, 48, 40, 4, 2, 6, mode=mode, kernel=0)
+    for fpl in (1, 6):
+        wf, sw = gpu_render(sc, 48, 40, 4, 2, 6, mode=mode, kernel=1, frames_per_launch=fpl)
+        np.testing.assert_array_equal(wf, mega)
+        assert sw["segments"] == sm["segments"]
+    if n_lights == 0:
+        assert np.all(mega == 0)
+    else:
+        o, segs = oracle_render(sc, 48, 40, 4, 2, 6, mode=mode)
+        np.testing.assert_array_equal(mega, o)
+
+
 @pytest.mark.parametrize("mode", [1, 0])
 def test_trace_kernel_timing_counts_every_launch(mode):
     """pt_set_kernel_timing brackets every trace launch with an event pair (bench.py's
@@ -463,7 +489,7 @@ def test_launch_params_matches_render():
 @pytest.mark.parametrize("mode", [1, 0])
 def test_fullhd_largest_batch_bit_identical(diffuse_scene, mode):
     """Maximum queue size at the headline resolution: 1920x1080 with frames_per_launch far
-    above the renderer's cap of 2^28 paths per batch (129 frames, 45 GB of queues: one batch of
+    above the renderer's cap of 2^28 paths per batch (129 frames, 56 GB of queues: one batch of
     129 frames and a ragged one of 1) gives the accumulator of 64-frame batches (64 + 64 + 2)
     bit for bit, with the same segment count."""
     n = 130
