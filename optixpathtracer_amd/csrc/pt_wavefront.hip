@@ -218,9 +218,22 @@ constexpr int kItemBits = 28;  // a queue item index is < 2^28 (kMaxWFPaths); th
 
 // Paths of nf consecutive frames are in flight together (path q = f * P + pixel), so every
 // launch works on nf frames' queues: fewer launches and one SIMT tail per nf frames.
-__global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame0, int nf) {
+// lean (fused modes with the primary dedup): k_extend traces only frame 0's camera rays and the
+// bounce-0 k_shade_fused derives the rest of the path state itself (shade0), so only frame 0's
+// rays are written -- the other frames' copies, throughputs and radiances are never read.
+__global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame0, int nf, int lean) {
     const int P = L.width * L.height;
     const int Q = P * nf;
+    if (lean) {
+        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P; q += gridDim.x * blockDim.x) {
+            f3 o, d;
+            camera_ray(L, q % L.width, q / L.width, o, d);
+            W.ray_o[0][q] = make_float4(o.x, o.y, o.z, __int_as_float(q));
+            W.ray_d[0][q] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kQueue) = Q;
+        return;
+    }
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += gridDim.x * blockDim.x) {
         const int f = q / P, p = q - f * P;
         const int x = p % L.width, y = p / L.width;
@@ -457,8 +470,13 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt(W, 0, kShadowQ) = n;
 }
 
-template <int MODE, bool TEX>
+// shade0 (bounce 0 after a lean k_camera): the path state is the camera's -- throughput 1, seed
+// tea16(pixel, frame) (devicePrograms.cu:631), radiance 0, direction that of the pixel's frame-0
+// ray (queue 0 is in path order) -- so it is derived here instead of read, and every path's
+// radiance is written rather than updated.
+template <int MODE, bool TEX, bool SHADE0>
 __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+    constexpr bool shade0 = SHADE0;
     // Lambert (memory-bound, 56 VGPRs): the throughput in queue order (queue_beta), +1.6 %; the
     // Conductor and Dielectric kernels are register-bound, and holding it across the appends
     // cost them 1-2 %, so they gather it by path
@@ -477,20 +495,27 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
         uint32_t seed = 0;
         float stmax = 0.0f;
         int path = 0;
+        const int P1 = L.width * L.height;
+        float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // shade0: the path's radiance after bounce 0
         if (valid) {
             const float4 hv = ldqs(W.hit + i);
             path = __float_as_int(hv.x);
             const Hit h = decode_hit(hv);
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
-                const float4 c = ldqs(rd + i);
+                const float4 c = ldqs(rd + (shade0 ? path % P1 : i));
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
-                float4 bv = ldqs(kBetaQ ? queue_beta(W, b) + i : W.beta + path);
-                seed = __float_as_uint(bv.w);
-                beta = mk(bv.x, bv.y, bv.z);
+                if (shade0) {
+                    seed = tea16((uint32_t)(path % P1), L.frame_base + (uint32_t)(path / P1));
+                    beta = mk(1.0f, 1.0f, 1.0f);
+                } else {
+                    float4 bv = ldqs(kBetaQ ? queue_beta(W, b) + i : W.beta + path);
+                    seed = __float_as_uint(bv.w);
+                    beta = mk(bv.x, bv.y, bv.z);
+                }
                 if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
-                    const float4 l = W.L[path];
+                    const float4 l = shade0 ? l0 : W.L[path];
                     debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, beta, mk(l.x, l.y, l.z));
                 }
                 const bool conductor = rnd(seed) < sf.metallic;  // :400
@@ -512,8 +537,9 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                         contrib = ((beta * spectrum) * Li) / (P * 1.0f);
                         if (vis0) {  // bounce 0: the (pixel, light) visibility is already known
                             if (W.vis[vis0_index(L, path, li)]) {
-                                const float4 l = W.L[path];
-                                W.L[path] = make_float4(l.x + contrib.x, l.y + contrib.y, l.z + contrib.z, 0.0f);
+                                const float4 l = shade0 ? l0 : W.L[path];
+                                l0 = make_float4(l.x + contrib.x, l.y + contrib.y, l.z + contrib.z, 0.0f);
+                                if (!shade0) W.L[path] = l0;
                             }
                         } else {
                             so = sf.pos + 1e-3f * sf.ng;
@@ -532,6 +558,7 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
                 }
             }
         }
+        if (shade0 && valid) W.L[path] = l0;  // every path of the batch, hit or miss
         const int si = block_append(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
         if (emit_shadow) {
             stqs(W.sh_o + si, make_float4(so.x, so.y, so.z, __int_as_float(path)));
@@ -916,11 +943,17 @@ dim3 occupancy_grid(K kernel, int cus) {
 // phase (Default / Layered): 0 = k_shade_a, 1 = k_shade_nee, 2 = k_shade_smp
 template <int MODE, bool TEX>
 hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
-                          hipStream_t stream, int phase, int vis0) {
+                          hipStream_t stream, int phase, int vis0, int shade0) {
     if (fused) {
         if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
-            hipLaunchKernelGGL((k_shade_fused<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L,
-                               W, b, vis0);
+        {
+            if (shade0)
+                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, true>), item_grid(items, kBlockSh), dim3(kBlockSh), 0,
+                                   stream, S, L, W, b, vis0);
+            else
+                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, false>), item_grid(items, kBlockSh), dim3(kBlockSh), 0,
+                                   stream, S, L, W, b, vis0);
+        }
     } else if (phase == 0) {
         hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b,
                            vis0);
@@ -936,20 +969,20 @@ hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, con
 
 template <int MODE>
 hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
-                        hipStream_t stream, int phase, int vis0) {
-    return S.texinfo ? launch_shade_t<MODE, true>(fused, S, L, W, b, items, stream, phase, vis0)
-                     : launch_shade_t<MODE, false>(fused, S, L, W, b, items, stream, phase, vis0);
+                        hipStream_t stream, int phase, int vis0, int shade0) {
+    return S.texinfo ? launch_shade_t<MODE, true>(fused, S, L, W, b, items, stream, phase, vis0, shade0)
+                     : launch_shade_t<MODE, false>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
 }
 
 // vis0: n_lights when the bounce-0 (pixel, light) visibility table is used at this bounce, else 0
 hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b,
-                             int items, hipStream_t stream, int phase, int vis0) {
+                             int items, hipStream_t stream, int phase, int vis0, int shade0 = 0) {
     switch (mode) {
-        case kModeLambert: return launch_shade<kModeLambert>(fused, S, L, W, b, items, stream, phase, vis0);
-        case kModeConductor: return launch_shade<kModeConductor>(fused, S, L, W, b, items, stream, phase, vis0);
-        case kModeDielectric: return launch_shade<kModeDielectric>(fused, S, L, W, b, items, stream, phase, vis0);
-        case kModeLayered: return launch_shade<kModeLayered>(fused, S, L, W, b, items, stream, phase, vis0);
-        default: return launch_shade<kModeDefault>(fused, S, L, W, b, items, stream, phase, vis0);
+        case kModeLambert: return launch_shade<kModeLambert>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
+        case kModeConductor: return launch_shade<kModeConductor>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
+        case kModeDielectric: return launch_shade<kModeDielectric>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
+        case kModeLayered: return launch_shade<kModeLayered>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
+        default: return launch_shade<kModeDefault>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
     }
 }
 
@@ -1009,7 +1042,10 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_camera, item_grid(P, kBlockWF), dim3(kBlockWF), 0, stream, W, L, frame, nf);
+    // fused modes with the primary dedup: frame 0's camera rays only (k_camera `lean`, shade0)
+    const bool lean = fused_mode(mode) && primary_dedup && nf > 1 && maxb > 0;
+    hipLaunchKernelGGL(k_camera, item_grid(lean ? L.width * L.height : P, kBlockWF), dim3(kBlockWF), 0, stream, W, L,
+                       frame, nf, lean ? 1 : 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const bool fused = fused_mode(mode);
     const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
@@ -1090,7 +1126,8 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         if ((e = extend(0, primary_dedup ? nf : 1)) != hipSuccess) return e;
         if ((e = shadow0()) != hipSuccess) return e;
         for (int b = 0; b < maxb; ++b) {
-            if ((e = launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0)) != hipSuccess)
+            if ((e = launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0, b == 0 && lean)) !=
+                hipSuccess)
                 return e;
             if ((e = pair(b)) != hipSuccess) return e;
         }
