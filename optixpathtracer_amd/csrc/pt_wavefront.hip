@@ -481,6 +481,7 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
     // Conductor and Dielectric kernels are register-bound, and holding it across the appends
     // cost them 1-2 %, so they gather it by path
     constexpr bool kBetaQ = MODE == kModeLambert;
+    constexpr bool kShareOrigin = MODE == kModeLambert;
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
@@ -559,17 +560,22 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
             }
         }
         if (shade0 && valid) W.L[path] = l0;  // every path of the batch, hit or miss
-        const int si = block_append(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
-        if (emit_shadow) {
-            stqs(W.sh_o + si, make_float4(so.x, so.y, so.z, __int_as_float(path)));
-            stqs(W.sh_d + si, make_float4(sdir.x, sdir.y, sdir.z, stmax));
-            stqs(W.sh_c + si, make_float4(contrib.x, contrib.y, contrib.z, 0.0f));
-        }
         const int qi = block_append(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
             if (kBetaQ) stqs(queue_beta(W, b + 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
+        }
+        const int si = block_append(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
+        if (emit_shadow) {
+            // Lambert: a sampled direction is never below the surface (lambert_sample forces z >= 0),
+            // so the continuation ray starts at the shadow ray's origin (sf.pos + 1e-3 * Ng, the
+            // same expression): the shadow record names that ray (qi) instead of repeating origin
+            // and path, and k_trace_pair reads them from the extension queue.  -1: own sh_o record.
+            const bool share = kShareOrigin && emit_next;
+            if (!share) stqs(W.sh_o + si, make_float4(so.x, so.y, so.z, __int_as_float(path)));
+            stqs(W.sh_d + si, make_float4(sdir.x, sdir.y, sdir.z, stmax));
+            stqs(W.sh_c + si, make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(share ? qi : -1)));
         }
     }
 }
@@ -599,12 +605,15 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
             st.path = __float_as_int(a.w);
         } else {
             const int j = i - n_ext;
-            const float4 a = W.sh_o[j], c = W.sh_d[j];
+            const float4 c = W.sh_d[j], k = W.sh_c[j];
+            // origin | path: the shadow ray's own record, or (Lambert) the continuation ray of the
+            // same path, which starts at the same point (k_shade_fused)
+            const int q = __float_as_int(k.w);
+            const float4 a = q >= 0 ? ro[q] : W.sh_o[j];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
             st.any = true;
             // an any-hit traversal only writes h.tri: the record's other fields carry the path
             // and the contribution to finish()
-            const float4 k = W.sh_c[j];
             st.h.orig = __float_as_int(a.w);
             st.h.t = k.x;
             st.h.u = k.y;
