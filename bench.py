@@ -269,7 +269,9 @@ def main():
         sj = ROOT / "profiles" / "shade_pmc.json"
         if sj.exists() and dom == "k_extend+k_trace_pair" and args.config == "2":
             try:
-                sk = json.loads(sj.read_text())["kernels"]["k_shade_fused<1, false>"]
+                ks = json.loads(sj.read_text())["kernels"]
+                # bounces >= 1 (the bounce-0 instance derives its path state, shade0)
+                sk = ks.get("k_shade_fused<1, false, false>") or ks["k_shade_fused<1, false>"]
                 shade = {"kernel": "k_shade_fused<Lambert>", **{k: sk[k] for k in ("hbm_gbps", "frac", "avg_launch_ms")}}
             except Exception:
                 shade = None
