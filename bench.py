@@ -226,6 +226,32 @@ def main():
             e1 = float(t.item())
         value_nodedup = args.width * args.height * per_step_spp / e1 / 1e6
         r.set_primary_dedup(True)
+    # Transparency: the timed steps alternate the wavefront batches between two streams
+    # (pt_set_wavefront_streams, default 2), so a trace launch shares the GPU with the other
+    # batch's kernels and its event window is longer than its solo run.  One more step on a
+    # single stream gives the trace kernels' solo launch time (roofline.single_stream).
+    single = None
+    if args.kernel != 0 and not args.no_dedup_check:
+        r.set_wavefront_streams(1)
+        r.stats_reset()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        step(args.warmup + args.steps + 1)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        e2 = time.perf_counter() - t2
+        s1 = r.stats()
+        if s1["trace_kernel_launches"] > 0:
+            l1 = int(s1["trace_kernel_launches"])
+            ms1 = s1["trace_kernel_ms"] / l1
+            ach1 = s1["trace_kernel_bytes"] / l1 / (ms1 / 1e3) / 1e9
+            single = {"value": round(args.width * args.height * per_step_spp / e2 / 1e6, 3),
+                      "avg_launch_ms": round(ms1, 4), "achieved": round(ach1, 2),
+                      "frac": round(ach1 / HBM_PEAK_GBPS, 5), "launches": l1}
+        r.set_wavefront_streams(2)
     if rank == 0:
         nan_px = int(np.isnan(img).any(axis=-1).sum())
         kernel_s = st["total_render_ms"] / 1e3
@@ -329,6 +355,7 @@ def main():
                 "valu_pmc": valu,
                 # PMC HBM bandwidth of the shading kernel (2 x FETCH_SIZE + WRITE_SIZE per launch)
                 "shade_pmc": shade,
+                "single_stream": single,
             },
             "image": {"mean": float(np.nanmean(img) / per_step_spp), "nan_pixels": nan_px},
         }

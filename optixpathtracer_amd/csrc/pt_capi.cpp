@@ -94,6 +94,12 @@ constexpr int kMinTraversalStack = 16 + kSpillDepth;  // pt_wavefront.hip kStack
 struct pt_renderer {
     int device = 0;
     hipStream_t stream = nullptr;
+    // wavefront batches alternate between two streams, each with its own queues, so one batch's
+    // kernels overlap the other's (pt_set_wavefront_streams; 1 = everything on `stream`)
+    int wf_streams = 2;
+    hipStream_t stream2 = nullptr;
+    WFState wf2;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_accum[2] = {nullptr, nullptr};
     // scene
     BNode4* d_nodes = nullptr;
     float4* d_isect = nullptr;
@@ -245,19 +251,46 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         const int P = r->width * r->height;
         const int nf_cap = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
                                                  kMaxWFPaths / std::max(1, P)}));
-        if (r->wf.paths < P * nf_cap || r->wf.max_bounces < r->max_bounces) {
-            PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
-            wavefront_free(r->wf);
-            PT_HIP(wavefront_alloc(r->wf, P * nf_cap, std::max(1, r->max_bounces)), "wavefront_alloc");
+        // two batches or more: alternate them between two streams with their own queues, so one
+        // batch's kernels run beside the other's (the memory-bound shading of one beside the
+        // VALU-bound tracing of the other, and each kernel's SIMT tail filled); k_accum still adds
+        // the batches in frame order (accum_wait / accum_done)
+        const bool dual = r->wf_streams > 1 && n > (uint32_t)nf_cap;
+        for (int k = 0; k < (dual ? 2 : 1); ++k) {
+            WFState& w = k ? r->wf2 : r->wf;
+            if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces) {
+                PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+                if (r->stream2) PT_HIP(hipStreamSynchronize(r->stream2), "hipStreamSynchronize");
+                wavefront_free(w);
+                PT_HIP(wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces)), "wavefront_alloc");
+            }
+        }
+        if (dual && !r->stream2) {
+            PT_HIP(hipStreamCreateWithFlags(&r->stream2, hipStreamNonBlocking), "hipStreamCreate");
+            PT_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming), "hipEventCreate");
+            PT_HIP(hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming), "hipEventCreate");
+            for (hipEvent_t& e : r->ev_accum) PT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
         }
         int dev_cus = 256;
         (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, r->device);
-        for (uint32_t f = 0; f < n;) {  // one event pair per batch (the batch's kernel chain)
-            const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
-            DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf, accum64);
-            hipEvent_t a, b;
+        hipEvent_t a = nullptr, b = nullptr;  // dual: one event pair around the whole call
+        if (dual) {
             rc = next_event_pair(r, &a, &b);
             if (rc) return rc;
+            PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
+            PT_HIP(hipEventRecord(r->ev_fork, r->stream), "hipEventRecord");
+            PT_HIP(hipStreamWaitEvent(r->stream2, r->ev_fork, 0), "hipStreamWaitEvent");
+        }
+        int batch = 0;
+        for (uint32_t f = 0; f < n; ++batch) {  // one event pair per batch (the batch's kernel chain)
+            const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
+            DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf, accum64);
+            const bool second = dual && (batch & 1);
+            hipStream_t st = second ? r->stream2 : r->stream;
+            if (!dual) {
+                rc = next_event_pair(r, &a, &b);
+                if (rc) return rc;
+            }
             const hipEvent_t* tev = nullptr;
             if (r->kernel_timing) {
                 r->tev_frame.resize(2 * (size_t)(r->max_bounces + 1));  // <= max_bounces + 1 trace launches
@@ -265,15 +298,21 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                     PT_HIP(r->tev.next(&r->tev_frame[2 * k], &r->tev_frame[2 * k + 1]), "hipEventCreate");
                 tev = r->tev_frame.data();
             }
-            PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
+            if (!dual) PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
             int n_timed = 0;
-            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, r->wf, first + f, nf,
-                                          r->primary_dedup, dev_cus,
-                                          r->stream, tev, &n_timed),
+            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, second ? r->wf2 : r->wf, first + f,
+                                          nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
+                                          dual && batch > 0 ? r->ev_accum[(batch - 1) & 1] : nullptr,
+                                          dual ? r->ev_accum[batch & 1] : nullptr),
                    "wavefront launch");
             if (tev) r->tev.give_back((size_t)(r->max_bounces + 1 - n_timed));  // pairs never recorded
-            PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
+            if (!dual) PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
             f += (uint32_t)nf;
+        }
+        if (dual) {
+            PT_HIP(hipEventRecord(r->ev_join, r->stream2), "hipEventRecord");
+            PT_HIP(hipStreamWaitEvent(r->stream, r->ev_join, 0), "hipStreamWaitEvent");
+            PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
         }
         done = n;
     }
@@ -626,6 +665,10 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_counters) (void)hipFree(r->d_counters);
     if (r->d_debug) (void)hipFree(r->d_debug);
     wavefront_free(r->wf);
+    wavefront_free(r->wf2);
+    if (r->stream2) (void)hipStreamDestroy(r->stream2);
+    for (hipEvent_t e : {r->ev_fork, r->ev_join, r->ev_accum[0], r->ev_accum[1]})
+        if (e) (void)hipEventDestroy(e);
     r->ev.destroy();
     r->tev.destroy();
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -1209,6 +1252,16 @@ extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
     if (!r) return fail(PT_ERR_INVALID, "pt_set_traversal_stats: NULL");
     r->trav_stats = enable != 0;
     for (pt_renderer* p : r->peers) p->trav_stats = enable != 0;
+    return PT_OK;
+}
+
+extern "C" int pt_set_wavefront_streams(pt_renderer* r, int32_t streams) {
+    if (!r || streams < 1 || streams > 2) return fail(PT_ERR_INVALID, "pt_set_wavefront_streams: 1 or 2");
+    int rc = collect_pending(r);
+    if (rc != PT_OK) return rc;
+    r->wf_streams = streams;
+    for (pt_renderer* p : r->peers)
+        if ((rc = pt_set_wavefront_streams(p, streams)) != PT_OK) return rc;
     return PT_OK;
 }
 

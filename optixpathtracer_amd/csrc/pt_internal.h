@@ -66,10 +66,13 @@ void wavefront_free(WFState& W);
 // launches; *n_timed (optional) receives the number of event pairs recorded.
 // nf frames (frame .. frame + nf - 1) are traced together; W must hold nf * W * H paths.
 // primary_dedup: trace the batch's identical camera rays once per pixel (k_extend `dup`).
+// accum_wait / accum_done (optional): the batch's k_accum waits for accum_wait and records
+// accum_done, so batches on different streams still add into the sum in frame order.
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
                                   const hipEvent_t* trace_events,
-                                  int* n_timed = nullptr);
+                                  int* n_timed = nullptr, hipEvent_t accum_wait = nullptr,
+                                  hipEvent_t accum_done = nullptr);
 
 // Render launches.
 hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,

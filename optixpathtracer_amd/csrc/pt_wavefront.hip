@@ -1046,7 +1046,8 @@ void wavefront_free(WFState& W) {
 
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
-                                  const hipEvent_t* trace_events, int* n_timed) {
+                                  const hipEvent_t* trace_events, int* n_timed, hipEvent_t accum_wait,
+                                  hipEvent_t accum_done) {
     const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
@@ -1154,7 +1155,9 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
                 return e;
         }
     }
+    if (accum_wait && (e = hipStreamWaitEvent(stream, accum_wait, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
+    if (accum_done && (e = hipEventRecord(accum_done, stream)) != hipSuccess) return e;
     if (n_timed) *n_timed = timed;  // fused modes: max_bounces + 1; Default / Layered: max_bounces
     return hipGetLastError();
 }

@@ -202,6 +202,9 @@ class OptixRenderer:
     def set_primary_dedup(self, enable: bool) -> None:
         check(self.lib.pt_set_primary_dedup(self.h, 1 if enable else 0), "pt_set_primary_dedup")
 
+    def set_wavefront_streams(self, streams: int) -> None:
+        check(self.lib.pt_set_wavefront_streams(self.h, int(streams)), "pt_set_wavefront_streams")
+
     def render_accumulate(self, spp: int, first_frame_id: int = 1) -> np.ndarray:
         """Clear, render frame ids first_frame_id .. +spp-1 and return the mean image
         (pt_render_accumulate); the sum stays in the device accumulator."""

@@ -354,6 +354,41 @@ def test_shallow_depth_and_light_count(depth, mode, n_lights):
     assert abs(sw["segments"] - segs) <= 0.01 * segs + 2
 
 
+@pytest.mark.parametrize("mode", [1, 3, 0])
+def test_wavefront_two_streams_bit_identical(mode):
+    """pt_set_wavefront_streams(2) (the default) alternates the batches of a call between two
+    streams with their own queues; k_accum still adds the batches in frame order, so the sum --
+    fp32 and fp64 -- equals the one-stream sum bit for bit, also across calls and with the
+    trace-kernel timing on (11 frames = batches of 4 + 4 + 3)."""
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    sc = scenes.tiny_scene("conductor" if mode == 0 else "diffuse")
+    out = {}
+    for streams in (1, 2):
+        for fp64 in (False, True):
+            r = setup_renderer(sc, 48, 40, 5, kernel=1)
+            r.set_material_mode(mode)
+            r.set_frames_per_launch(4)
+            r.set_wavefront_streams(streams)
+            r.set_kernel_timing(True)
+            if fp64:
+                r.set_accum_fp64(True)
+            r.accum_clear()
+            r.render_frames(7, 11)
+            r.render_frames(18, 5)  # a second call continues the sum
+            out[streams, fp64] = (r.accum(), r.stats())
+            r.close()
+    for fp64 in (False, True):
+        (a, sa), (b, sb) = out[1, fp64], out[2, fp64]
+        np.testing.assert_array_equal(a, b)
+        assert sa["segments"] == sb["segments"]
+        assert sa["trace_kernel_launches"] == sb["trace_kernel_launches"] > 0
+    mega, _ = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=0)
+    one, _ = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=1, frames_per_launch=4)
+    np.testing.assert_array_equal(one, mega)
+
+
 @pytest.mark.parametrize("n_lights", [0, 1])
 @pytest.mark.parametrize("variant,mode", [("conductor", 0), ("layered", 4), ("conductor", 4), ("diffuse", 0)])
 def test_bucketed_shading_queues(variant, mode, n_lights):
