@@ -172,10 +172,10 @@ int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
  * hit record to every frame (default 1).  0 traces every frame's copy; the images are
  * bit-identical either way. */
 int pt_set_primary_dedup(pt_renderer* r, int32_t enable);
-/* Wavefront: streams the batches of a pt_render_frames call alternate between (1 or 2, default
- * 2).  With 2, consecutive batches run on two streams with their own queues, so one batch's
- * kernels overlap the other's; the batches still add into the sum in frame order, and the image
- * is bit-identical to 1.  A call of one batch uses one stream either way. */
+/* Wavefront: streams the batches of a pt_render_frames call alternate between (1 to 4, default
+ * 2).  With more than 1, consecutive batches run on different streams with their own queues, so
+ * one batch's kernels overlap another's; the batches still add into the sum in frame order, and
+ * the image is bit-identical to 1.  A call uses at most as many streams as it has batches. */
 int pt_set_wavefront_streams(pt_renderer* r, int32_t streams);
 
 /* LaunchParams (Renderer/OptiX/LaunchParams.h:9-28) as a C struct: the state one optixLaunch

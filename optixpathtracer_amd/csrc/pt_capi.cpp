@@ -96,10 +96,12 @@ struct pt_renderer {
     hipStream_t stream = nullptr;
     // wavefront batches alternate between two streams, each with its own queues, so one batch's
     // kernels overlap the other's (pt_set_wavefront_streams; 1 = everything on `stream`)
+    static constexpr int kMaxWFStreams = 4;
     int wf_streams = 2;
-    hipStream_t stream2 = nullptr;
-    WFState wf2;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_accum[2] = {nullptr, nullptr};
+    hipStream_t xstream[kMaxWFStreams] = {};  // [0] unused: stream 0 is `stream`
+    WFState xwf[kMaxWFStreams];               // [0] unused: stream 0's queues are `wf`
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxWFStreams] = {}, ev_accum[2] = {nullptr, nullptr};
+    hipStream_t wf_stream(int k) const { return k ? xstream[k] : stream; }
     // scene
     BNode4* d_nodes = nullptr;
     float4* d_isect = nullptr;
@@ -255,22 +257,27 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // batch's kernels run beside the other's (the memory-bound shading of one beside the
         // VALU-bound tracing of the other, and each kernel's SIMT tail filled); k_accum still adds
         // the batches in frame order (accum_wait / accum_done)
-        const bool dual = r->wf_streams > 1 && n > (uint32_t)nf_cap;
-        for (int k = 0; k < (dual ? 2 : 1); ++k) {
-            WFState& w = k ? r->wf2 : r->wf;
+        const int nbatch = (int)((n + (uint32_t)nf_cap - 1) / (uint32_t)nf_cap);
+        const int ns = std::max(1, std::min(r->wf_streams, nbatch));
+        const bool dual = ns > 1;
+        for (int k = 0; k < ns; ++k) {
+            WFState& w = k ? r->xwf[k] : r->wf;
             if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces) {
-                PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
-                if (r->stream2) PT_HIP(hipStreamSynchronize(r->stream2), "hipStreamSynchronize");
+                for (int j = 0; j < pt_renderer::kMaxWFStreams; ++j)
+                    if (r->wf_stream(j)) PT_HIP(hipStreamSynchronize(r->wf_stream(j)), "hipStreamSynchronize");
                 wavefront_free(w);
                 PT_HIP(wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces)), "wavefront_alloc");
             }
         }
-        if (dual && !r->stream2) {
-            PT_HIP(hipStreamCreateWithFlags(&r->stream2, hipStreamNonBlocking), "hipStreamCreate");
+        if (dual && !r->ev_fork) {
             PT_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming), "hipEventCreate");
-            PT_HIP(hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming), "hipEventCreate");
             for (hipEvent_t& e : r->ev_accum) PT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
         }
+        for (int k = 1; k < ns; ++k)
+            if (!r->xstream[k]) {
+                PT_HIP(hipStreamCreateWithFlags(&r->xstream[k], hipStreamNonBlocking), "hipStreamCreate");
+                PT_HIP(hipEventCreateWithFlags(&r->ev_join[k], hipEventDisableTiming), "hipEventCreate");
+            }
         int dev_cus = 256;
         (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, r->device);
         hipEvent_t a = nullptr, b = nullptr;  // dual: one event pair around the whole call
@@ -279,14 +286,14 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             if (rc) return rc;
             PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
             PT_HIP(hipEventRecord(r->ev_fork, r->stream), "hipEventRecord");
-            PT_HIP(hipStreamWaitEvent(r->stream2, r->ev_fork, 0), "hipStreamWaitEvent");
+            for (int k = 1; k < ns; ++k) PT_HIP(hipStreamWaitEvent(r->xstream[k], r->ev_fork, 0), "hipStreamWaitEvent");
         }
         int batch = 0;
         for (uint32_t f = 0; f < n; ++batch) {  // one event pair per batch (the batch's kernel chain)
             const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
             DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf, accum64);
-            const bool second = dual && (batch & 1);
-            hipStream_t st = second ? r->stream2 : r->stream;
+            const int sk = batch % ns;  // stream of this batch
+            hipStream_t st = r->wf_stream(sk);
             if (!dual) {
                 rc = next_event_pair(r, &a, &b);
                 if (rc) return rc;
@@ -300,7 +307,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             }
             if (!dual) PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
             int n_timed = 0;
-            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, second ? r->wf2 : r->wf, first + f,
+            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, sk ? r->xwf[sk] : r->wf, first + f,
                                           nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
                                           dual && batch > 0 ? r->ev_accum[(batch - 1) & 1] : nullptr,
                                           dual ? r->ev_accum[batch & 1] : nullptr),
@@ -310,8 +317,10 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             f += (uint32_t)nf;
         }
         if (dual) {
-            PT_HIP(hipEventRecord(r->ev_join, r->stream2), "hipEventRecord");
-            PT_HIP(hipStreamWaitEvent(r->stream, r->ev_join, 0), "hipStreamWaitEvent");
+            for (int k = 1; k < ns; ++k) {
+                PT_HIP(hipEventRecord(r->ev_join[k], r->xstream[k]), "hipEventRecord");
+                PT_HIP(hipStreamWaitEvent(r->stream, r->ev_join[k], 0), "hipStreamWaitEvent");
+            }
             PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
         }
         done = n;
@@ -665,9 +674,12 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_counters) (void)hipFree(r->d_counters);
     if (r->d_debug) (void)hipFree(r->d_debug);
     wavefront_free(r->wf);
-    wavefront_free(r->wf2);
-    if (r->stream2) (void)hipStreamDestroy(r->stream2);
-    for (hipEvent_t e : {r->ev_fork, r->ev_join, r->ev_accum[0], r->ev_accum[1]})
+    for (int k = 1; k < pt_renderer::kMaxWFStreams; ++k) {
+        wavefront_free(r->xwf[k]);
+        if (r->xstream[k]) (void)hipStreamDestroy(r->xstream[k]);
+        if (r->ev_join[k]) (void)hipEventDestroy(r->ev_join[k]);
+    }
+    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1]})
         if (e) (void)hipEventDestroy(e);
     r->ev.destroy();
     r->tev.destroy();
@@ -1256,7 +1268,8 @@ extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
 }
 
 extern "C" int pt_set_wavefront_streams(pt_renderer* r, int32_t streams) {
-    if (!r || streams < 1 || streams > 2) return fail(PT_ERR_INVALID, "pt_set_wavefront_streams: 1 or 2");
+    if (!r || streams < 1 || streams > pt_renderer::kMaxWFStreams)
+        return fail(PT_ERR_INVALID, "pt_set_wavefront_streams: 1 to 4");
     int rc = collect_pending(r);
     if (rc != PT_OK) return rc;
     r->wf_streams = streams;

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--builders", default="0", help="0 = PLOC, 1 = LBVH")
+    ap.add_argument("--streams", default="", help="wavefront streams to sweep (pt_set_wavefront_streams)")
     a = ap.parse_args()
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import setup_renderer
@@ -44,7 +45,9 @@ def main():
                           "bvh_depth": st["bvh_depth"]}), flush=True)
         for kernel in [int(k) for k in a.kernels.split(",")]:
             for mode in modes:
-                for fpl in [int(f) for f in a.fpl.split(",")]:
+                for fpl, nstr in [(int(f), int(x)) for f in a.fpl.split(",") for x in (a.streams.split(",") if a.streams else ["0"])]:
+                    if nstr:
+                        r.set_wavefront_streams(nstr)
                     r.set_kernel(kernel)
                     r.set_material_mode(mode)
                     r.set_frames_per_launch(fpl)
@@ -61,7 +64,8 @@ def main():
                         s = r.stats()
                         best = ms if best is None else min(best, ms)
                     samples = a.width * a.height * a.spp
-                    out = {"kernel": kernel, "mode": mode, "fpl": fpl, "wall_ms": round(best, 2),
+                    out = {"kernel": kernel, "mode": mode, "fpl": fpl, **({"streams": nstr} if nstr else {}),
+                           "wall_ms": round(best, 2),
                            "msamples_s": round(samples / best / 1e3, 2),
                            "segments_per_sample": round(s["segments"] / samples, 4)}
                     if a.stats:
