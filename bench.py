@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
                     help="PMC traffic per launch measured by tools/profile.sh (optional)")
+    ap.add_argument("--wavefront-streams", type=int, default=2,
+                    help="streams the wavefront batches alternate between (pt_set_wavefront_streams)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="override the config's scaling: strong = the step's spp in total, split over the "
                          "ranks (for configs[1]: the one 1024-spp headline image rendered by N GPUs)")
@@ -151,6 +153,7 @@ def main():
     t0 = time.perf_counter()
     r = setup_renderer(scene, args.width, args.height, args.depth, device=local_rank, kernel=args.kernel)
     r.set_frames_per_launch(args.frames_per_launch)
+    r.set_wavefront_streams(args.wavefront_streams)
     if args.kernel != 0:  # wavefront (auto resolves to it): time every k_extend launch
         r.set_kernel_timing(True)
     setup_s = time.perf_counter() - t0
@@ -231,7 +234,7 @@ def main():
     # batch's kernels and its event window is longer than its solo run.  One more step on a
     # single stream gives the trace kernels' solo launch time (roofline.single_stream).
     single = None
-    if args.kernel != 0 and not args.no_dedup_check:
+    if args.kernel != 0 and not args.no_dedup_check and args.wavefront_streams > 1:
         r.set_wavefront_streams(1)
         r.stats_reset()
         if dist is not None:
@@ -251,7 +254,7 @@ def main():
             single = {"value": round(args.width * args.height * per_step_spp / e2 / 1e6, 3),
                       "avg_launch_ms": round(ms1, 4), "achieved": round(ach1, 2),
                       "frac": round(ach1 / HBM_PEAK_GBPS, 5), "launches": l1}
-        r.set_wavefront_streams(2)
+        r.set_wavefront_streams(args.wavefront_streams)
     if rank == 0:
         nan_px = int(np.isnan(img).any(axis=-1).sum())
         kernel_s = st["total_render_ms"] / 1e3

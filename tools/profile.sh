@@ -14,6 +14,9 @@ cd "$ROOT"
 echo "[profile] kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
+echo "[profile] kernel trace, one stream (solo kernel times: tools/shade_pmc.py, roofline.single_stream)"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt1" -o run -- \
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --wavefront-streams 1 $ARGS > "$OUT/kt1_bench.json" 2> "$OUT/kt1_bench.log"
 echo "[profile] FETCH_SIZE"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
   python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check $ARGS > "$OUT/fetch.json" 2> "$OUT/fetch.log"

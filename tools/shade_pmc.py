@@ -6,6 +6,8 @@ of the same batch size (64 frames per launch).  Writes profiles/shade_pmc.json, 
 reports next to the trace-kernel roofline (k_shade_fused is the memory-bound kernel of a
 Lambert frame).
     python tools/shade_pmc.py [fetch.csv write.csv kernel_stats.csv] > profiles/shade_pmc.json
+(kernel_stats.csv: the one-stream pass, tools/profile.sh kt1 -- with two wavefront streams a
+shading launch shares the GPU with the other stream's trace kernels and its time is not its own)
 """
 import collections
 import csv

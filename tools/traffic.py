@@ -80,6 +80,8 @@ def main():
         "hbm_bytes_per_launch": int(hbm),
         "hbm_bytes_per_launch_low": int(low),
         "kernel_trace": stats.get(kernel),
+        # the same bench on one wavefront stream (tools/profile.sh kt1): solo launch times
+        "kernel_trace_single_stream": kernel_stats(root / "kt1").get(kernel) if (root / "kt1").exists() else None,
         "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes; low: FETCH_SIZE + "
                       "WRITE_SIZE (gathers are not half-counted, profiles/r02_hbm_calib.json)",
     }, indent=1))
