@@ -368,7 +368,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
 // copy; DESIGN.md §5 gives the A/B.
 template <bool STATS, bool TEX>
 __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_extend(DevScene S, WFState W, int b, int dup,
-                                                                  unsigned long long* counters) {
+                                                                  int copies, unsigned long long* counters) {
     __shared__ int stack[kStack * kBlockWF];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
     __shared__ TriBatchLds tri_batch[kTriBatchWaves];
@@ -388,14 +388,15 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_extend(DevScene S, 
             st.path = __float_as_int(a.w);
         },
         [&](int ri, const TravState& st) {
-            // copy k of a bounce-0 ray is path st.path + k * n_trace (queue 0 is in path order)
-            for (int k = 0; k < dup; ++k)
+            // copy k of a bounce-0 ray is path st.path + k * n_trace (queue 0 is in path order);
+            // copies = 1: k_shade0_pixel reads the pixel's one record for all its frames
+            for (int k = 0; k < copies; ++k)
                 W.hit[ri + (size_t)k * n_trace] = hit_record(st.h, st.path + k * n_trace);
         });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n);        // path segments
         atomicAdd(&counters[6], (unsigned long long)n_trace);  // rays traced by the timed trace kernels
-        atomicAdd(&counters[7], 32ull * (unsigned long long)n_trace + 16ull * (unsigned long long)n);  // bytes
+        atomicAdd(&counters[7], (32ull + 16ull * (unsigned long long)copies) * (unsigned long long)n_trace);  // bytes
     }
     flush_trav_stats<STATS>(counters, ts);
 }
@@ -576,6 +577,75 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
             if (!share) stqs(W.sh_o + si, make_float4(so.x, so.y, so.z, __int_as_float(path)));
             stqs(W.sh_d + si, make_float4(sdir.x, sdir.y, sdir.z, stmax));
             stqs(W.sh_c + si, make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(share ? qi : -1)));
+        }
+    }
+}
+
+// Bounce 0 of a fused-mode batch with the primary dedup and the (pixel, light) visibility table:
+// the nf paths of a pixel start from the same hit (no pixel jitter, devicePrograms.cu:601-623),
+// so one thread reconstructs the pixel's surface once and shades its paths in frame order (k_extend
+// wrote one hit record per pixel).  Per path: the operations of k_shade_fused<SHADE0> (throughput
+// 1, seed tea16(pixel, frame), radiance written, continuation appended to queue 1).
+template <int MODE, bool TEX>
+__global__ __launch_bounds__(kBlockSh, 1) void k_shade0_pixel(DevScene S, DevLaunch L, WFState W, int nf) {
+    constexpr bool kBetaQ = MODE == kModeLambert;  // as k_shade_fused
+    const int P1 = L.width * L.height;
+    __shared__ int lds_q[kWavesSh + 1];
+    if ((int)(blockIdx.x * kBlockSh) >= P1) return;  // block-uniform
+    const int p = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+    const bool valid = p < P1;
+    int tri = -1;
+    SurfaceHit sf;
+    if (valid) {
+        const float4 hv = W.hit[p];
+        const Hit h = decode_hit(hv);
+        tri = h.tri;
+        if (tri >= 0) {
+            const float4 c = W.ray_d[0][p];
+            reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
+        }
+    }
+    const int dbg = debug_path_id(L);
+    float4* no = W.ray_o[1];
+    float4* nd = W.ray_d[1];
+    for (int f = 0; f < nf; ++f) {  // uniform trip count (block_append below)
+        const int path = f * P1 + p;
+        bool emit_next = false;
+        f3 o, d, beta = mk(1.0f, 1.0f, 1.0f);
+        uint32_t seed = 0;
+        float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (valid && tri >= 0) {
+            seed = tea16((uint32_t)p, L.frame_base + (uint32_t)f);  // devicePrograms.cu:631
+            if (path == dbg) debug_record(L, 1, __float_as_int(S.isect[3 * tri].w), sf, beta, mk(0.0f, 0.0f, 0.0f));
+            const bool conductor = rnd(seed) < sf.metallic;  // :400
+            int li;
+            const float P = pick_light(L, seed, li);
+            if (P > 0.0f) {
+                const DevLight lt = L.lights[li];
+                f3 lpos = mk(lt.px, lt.py, lt.pz);
+                f3 lds = to_local(sf.fr, normalize(lpos - sf.pos));
+                f3 fv = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, lds);
+                f3 spectrum = fv * abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+                if (!is_zero(spectrum) && W.vis[vis0_index(L, path, li)]) {
+                    f3 dd = sf.pos - lpos;
+                    float d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+                    f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+                    f3 contrib = ((beta * spectrum) * Li) / (P * 1.0f);
+                    l0 = make_float4(0.0f + contrib.x, 0.0f + contrib.y, 0.0f + contrib.z, 0.0f);
+                }
+            }
+            BSample bs;
+            if (1 < L.max_bounces && bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, conductor, sf.wo, bs)) {
+                emit_next = continue_path(sf, bs, beta, o, d, 1, L.max_bounces);
+                if (!kBetaQ) stqs(W.beta + path, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
+            }
+        }
+        if (valid) stqs(W.L + path, l0);  // every path of the batch, hit or miss
+        const int qi = block_append(cnt(W, 1, kQueue), emit_next, lds_q);
+        if (emit_next) {
+            stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
+            stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
+            if (kBetaQ) stqs(queue_beta(W, 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
         }
     }
 }
@@ -983,6 +1053,24 @@ hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const
                      : launch_shade_t<MODE, false>(fused, S, L, W, b, items, stream, phase, vis0, shade0);
 }
 
+template <int MODE>
+hipError_t launch_shade0_pixel_t(const DevScene& S, const DevLaunch& L, const WFState& W, int nf, hipStream_t stream) {
+    const dim3 grid = item_grid(L.width * L.height, kBlockSh);
+    if (S.texinfo)
+        hipLaunchKernelGGL((k_shade0_pixel<MODE, true>), grid, dim3(kBlockSh), 0, stream, S, L, W, nf);
+    else
+        hipLaunchKernelGGL((k_shade0_pixel<MODE, false>), grid, dim3(kBlockSh), 0, stream, S, L, W, nf);
+    return hipGetLastError();
+}
+hipError_t launch_shade0_pixel(int mode, const DevScene& S, const DevLaunch& L, const WFState& W, int nf,
+                               hipStream_t stream) {
+    switch (mode) {
+        case kModeLambert: return launch_shade0_pixel_t<kModeLambert>(S, L, W, nf, stream);
+        case kModeConductor: return launch_shade0_pixel_t<kModeConductor>(S, L, W, nf, stream);
+        default: return launch_shade0_pixel_t<kModeDielectric>(S, L, W, nf, stream);
+    }
+}
+
 // vis0: n_lights when the bounce-0 (pixel, light) visibility table is used at this bounce, else 0
 hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b,
                              int items, hipStream_t stream, int phase, int vis0, int shade0 = 0) {
@@ -1060,22 +1148,22 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     const bool fused = fused_mode(mode);
     const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
     int timed = 0;                          // trace launches bracketed by trace_events
-    auto extend = [&](int b, int dup) -> hipError_t {
+    auto extend = [&](int b, int dup, int copies) -> hipError_t {
         hipError_t r;
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
         if (tex) {
             if (stats)
                 hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockWF),
-                                   0, stream, S, W, b, dup, L.counters);
+                                   0, stream, S, W, b, dup, copies, L.counters);
             else
                 hipLaunchKernelGGL((k_extend<false, true>), occupancy_grid(k_extend<false, true>, cus),
-                                   dim3(kBlockWF), 0, stream, S, W, b, dup, L.counters);
+                                   dim3(kBlockWF), 0, stream, S, W, b, dup, copies, L.counters);
         } else if (stats) {
             hipLaunchKernelGGL((k_extend<true, false>), occupancy_grid(k_extend<true, false>, cus), dim3(kBlockWF), 0,
-                               stream, S, W, b, dup, L.counters);
+                               stream, S, W, b, dup, copies, L.counters);
         } else {
             hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockWF),
-                               0, stream, S, W, b, dup, L.counters);
+                               0, stream, S, W, b, dup, copies, L.counters);
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
         ++timed;
@@ -1133,17 +1221,23 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         // SamplePath's loop never runs (devicePrograms.cu:646): black frames, no segments
     } else if (fused) {
         // extend(0); then per bounce: shade(b) -> [shadow rays of b + extension rays of b+1]
-        if ((e = extend(0, primary_dedup ? nf : 1)) != hipSuccess) return e;
+        // lean bounce 0 with the visibility table: one hit record and one surface per pixel
+        const bool pixel0 = lean && vis0;
+        if ((e = extend(0, primary_dedup ? nf : 1, pixel0 ? 1 : (primary_dedup ? nf : 1))) != hipSuccess) return e;
         if ((e = shadow0()) != hipSuccess) return e;
         for (int b = 0; b < maxb; ++b) {
-            if ((e = launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0, b == 0 && lean)) !=
-                hipSuccess)
+            if (b == 0 && pixel0) {
+                if ((e = launch_shade0_pixel(mode, S, L, W, nf, stream)) != hipSuccess) return e;
+            } else if ((e = launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0, b == 0 && lean)) !=
+                       hipSuccess) {
                 return e;
+            }
             if ((e = pair(b)) != hipSuccess) return e;
         }
     } else {
         for (int b = 0; b < maxb; ++b) {
-            if ((e = extend(b, b == 0 && primary_dedup ? nf : 1)) != hipSuccess) return e;
+            const int dup = b == 0 && primary_dedup ? nf : 1;
+            if ((e = extend(b, dup, dup)) != hipSuccess) return e;
             const int v0 = b == 0 ? vis0 : 0;
             if (v0 && (e = shadow0()) != hipSuccess) return e;
             // k_shade_a queues the bounce's items by bucket; the visible ones (the bounce-0 table,
