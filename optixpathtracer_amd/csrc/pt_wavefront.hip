@@ -1016,7 +1016,12 @@ dim3 occupancy_grid(K kernel, int cus) {
     } else {
         per_cu = it->second;
     }
-    return dim3((unsigned)(per_cu * std::max(1, cus)));
+// (2x / 4x oversubscribed trace grids with the two wavefront streams: Lambert +0.2 / +0.5 %,
+// Dielectric +1.7 / +1.4 %, Layered -0.4 %: noise-level)
+#ifndef PT_TRACE_OVERSUB
+#define PT_TRACE_OVERSUB 1
+#endif
+    return dim3((unsigned)(PT_TRACE_OVERSUB * per_cu * std::max(1, cus)));
 }
 
 // phase (Default / Layered): 0 = k_shade_a, 1 = k_shade_nee, 2 = k_shade_smp
