@@ -560,8 +560,7 @@ __device__ __forceinline__ void wave_tri_batch(const DevScene& S, TravState& s, 
         s.leaf = kEmptyChild;
     }
     L->key[lane] = ~0ull;
-    const int flags = (s.strict ? 1 : 0) | (is_any<ANY>(s) ? 2 : 0);
-    const bool any_strict = __ballot(has && s.strict) != 0;
+    const int flags = is_any<ANY>(s) ? 2 : 0;
     __builtin_amdgcn_wave_barrier();
     for (int base = 0; base < total; base += 64) {  // total is wave-uniform
         const int k = base + lane;
@@ -571,20 +570,28 @@ __device__ __forceinline__ void wave_tri_batch(const DevScene& S, TravState& s, 
         const f3 o = mk(__shfl(s.o.x, owner, 64), __shfl(s.o.y, owner, 64), __shfl(s.o.z, owner, 64));
         const f3 d = mk(__shfl(s.d.x, owner, 64), __shfl(s.d.y, owner, 64), __shfl(s.d.z, owner, 64));
         const float tmax = __shfl(s.best, owner, 64);
-        const int fl = __shfl(flags, owner, 64);
         bool hit = false, bk = false;
         float t = 0.0f, u = 0.0f, v = 0.0f;
         int oi = 0;
+        float4 A = make_float4(0.0f, 0.0f, 0.0f, 0.0f), E1 = A, E2 = A;
         if (valid) {
             if (STATS) ts.tris++;
-            const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+            A = S.isect[3 * ti];
+            E1 = S.isect[3 * ti + 1];
+            E2 = S.isect[3 * ti + 2];
             hit = tri_test(A, E1, E2, o, d, 0.0f, tmax, t, u, v, bk);
             if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
-            if (any_strict && (fl & 1) && hit) {  // re-trace lanes only (rare): the owner's inv / io, recomputed
-                const f3 inv = safe_inv(d);
-                hit = tri_accept(A, E1, E2, inv, mk(o.x * inv.x, o.y * inv.y, o.z * inv.z), t);
-            }
             oi = __float_as_int(A.w);
+        }
+        // Every candidate is held to the acceptance rule here (tri_accept with the owner's inv / io,
+        // read across lanes by the whole wave), so the batch only ever takes acceptable hits: the
+        // traversal is strict from the start and its finished rays need no check and no re-trace.
+        // (Round 2 checked the finished rays' hits in the trace loop's refill block instead, which
+        // loaded each hit triangle again and stalled the block: +3.3 % Lambert)
+        if (__ballot(hit)) {  // wave-uniform
+            const f3 inv = mk(__shfl(s.inv.x, owner, 64), __shfl(s.inv.y, owner, 64), __shfl(s.inv.z, owner, 64));
+            const f3 io = mk(__shfl(s.io.x, owner, 64), __shfl(s.io.y, owner, 64), __shfl(s.io.z, owner, 64));
+            if (hit) hit = tri_accept(A, E1, E2, inv, io, t);
         }
         // t >= tmin = 0: with the sign bit cleared (t = -0), its bits order as an unsigned integer
         const unsigned long long key =
@@ -655,8 +662,9 @@ __device__ __forceinline__ bool trav_node_step(const DevScene& S, TravState& s, 
     return s.cur == kEmptyChild && s.leaf == kEmptyChild;
 }
 
-// A finished traversal's answer stands unless its hit is not acceptable (tri_accept) -- then
-// the ray is traced again in strict mode.  If the final hit is acceptable it IS the minimum
+// Per-lane traversals (trav_step: the megakernel and k_trace; the wavefront's triangle batches
+// are strict throughout): a finished traversal's answer stands unless its hit is not acceptable
+// (tri_accept) -- then the ray is traced again in strict mode.  If the final hit is acceptable it IS the minimum
 // over the acceptable hits: every acceptable hit ordered before it had t <= best throughout,
 // so its boxes were never culled and it was tested and taken.  It runs once per finished ray,
 // on the hit's t kept by the traversal and the hit triangle's record (A, E1, E2).

@@ -284,13 +284,12 @@ __device__ __forceinline__ void stqs(float4* p, float4 v) {
 
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.  A lane whose traversal ends parks
-// (`done`) until enough lanes are idle; then the wave runs one batch block that checks the
-// parked results (trav_result_ok: a rare unacceptable hit sends its lane back into a strict
-// re-trace instead), finishes them and refills the idle lanes with the next rays of the
-// slice.  Closest-hit lanes trace in [0, tmax_closest].
+// (`done`) until enough lanes are idle; then the wave runs one batch block that finishes the
+// parked rays and refills the idle lanes with the next rays of the slice.  The triangle
+// batches take acceptable hits only (wave_tri_batch), so a finished ray's answer is final.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
-__device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, float tmax_closest, int* stk,
-                                            TriBatchLds* tri_lds, TravStats& ts, Fetch fetch, Finish finish) {
+__device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TriBatchLds* tri_lds,
+                                            TravStats& ts, Fetch fetch, Finish finish) {
     int spill[kSpillDepth];
     TravState st;
     int ri = -1;
@@ -305,14 +304,9 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         // at every step once the slice is drained
         if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
             if (STATS) ts.refills++;
-            if (done) {
-                if (trav_result_ok<ANY, TEX>(S, st)) {
-                    finish(ri, st);
-                    ri = -1;
-                } else {
-                    trav_restart_strict<ANY>(st, tmax_closest);
-                    if (STATS) ts.retrace++;
-                }
+            if (done) {  // the triangle batches took acceptable hits only: the answer stands
+                finish(ri, st);
+                ri = -1;
                 done = false;
             }
             const unsigned long long m = __ballot(ri < 0);
@@ -358,7 +352,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, int* stk, 
                                             Fetch fetch, Finish finish) {
     int next, end;
     wave_slice(n, next, end);
-    trace_range<ANY, STATS, TEX>(S, next, end, 100.0f, stk, tri_lds, ts, fetch, finish);
+    trace_range<ANY, STATS, TEX>(S, next, end, stk, tri_lds, ts, fetch, finish);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -705,7 +699,7 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
     // per-wave shares of both kinds were slower).
     int first, end;
     wave_slice(n_ext + n_sh, first, end);
-    trace_range<kRayMixed, STATS, TEX>(S, first, end, 100.0f, stk, tri_lds, ts, fetch, finish);
+    trace_range<kRayMixed, STATS, TEX>(S, first, end, stk, tri_lds, ts, fetch, finish);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
