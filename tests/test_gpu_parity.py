@@ -365,7 +365,7 @@ def test_wavefront_two_streams_bit_identical(mode):
 
     sc = scenes.tiny_scene("conductor" if mode == 0 else "diffuse")
     out = {}
-    for streams in (1, 2):
+    for streams in (1, 2, 3):
         for fp64 in (False, True):
             r = setup_renderer(sc, 48, 40, 5, kernel=1)
             r.set_material_mode(mode)
@@ -380,10 +380,18 @@ def test_wavefront_two_streams_bit_identical(mode):
             out[streams, fp64] = (r.accum(), r.stats())
             r.close()
     for fp64 in (False, True):
-        (a, sa), (b, sb) = out[1, fp64], out[2, fp64]
-        np.testing.assert_array_equal(a, b)
-        assert sa["segments"] == sb["segments"]
-        assert sa["trace_kernel_launches"] == sb["trace_kernel_launches"] > 0
+        for streams in (2, 3):
+            (a, sa), (b, sb) = out[1, fp64], out[streams, fp64]
+            np.testing.assert_array_equal(a, b)
+            assert sa["segments"] == sb["segments"]
+            assert sa["trace_kernel_launches"] == sb["trace_kernel_launches"] > 0
+    from optixpathtracer_amd.capi import PTError
+
+    r = setup_renderer(sc, 16, 16, 2, kernel=1)
+    for bad in (0, 5, -1):  # 1 to 4 streams
+        with pytest.raises(PTError):
+            r.set_wavefront_streams(bad)
+    r.close()
     mega, _ = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=0)
     one, _ = gpu_render(sc, 48, 40, 5, 7, 11, mode=mode, kernel=1, frames_per_launch=4)
     np.testing.assert_array_equal(one, mega)
