@@ -87,7 +87,7 @@ struct EventPool {
 // overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces
 // [9..13] wave schedule of the trace kernels (pt_stats wave_*).
 constexpr int kCounters = 16;
-constexpr int kMinTraversalStack = 16 + kSpillDepth;  // pt_wavefront.hip kStack + pt_device.h kSpillDepth
+constexpr int kMinTraversalStack = 14 + kSpillDepth;  // pt_wavefront.hip kStack + pt_device.h kSpillDepth
 
 }  // namespace
 
@@ -609,7 +609,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         r->bvh_nodes = bo.n_nodes;
         r->bvh_depth = bo.depth;
         // a traversal holds at most 3 stack entries per BVH4 level; the smallest traversal stack
-        // (wavefront: 16 LDS + 64 spill entries) must hold them, or rays could lose subtrees
+        // (wavefront: 14 LDS + 64 spill entries) must hold them, or rays could lose subtrees
         if (3 * bo.depth > kMinTraversalStack)
             return cleanup_fail(fail(PT_ERR_INVALID, "pt_create: BVH too deep for the traversal stack (depth " +
                                                          std::to_string(bo.depth) + ")"));

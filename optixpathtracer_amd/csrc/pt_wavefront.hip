@@ -38,19 +38,20 @@ namespace pt {
 namespace {
 
 constexpr int kBlockWF = 256;
-// LDS traversal stack entries per lane: 16 KB per workgroup keeps the trace kernels
+// LDS traversal stack entries per lane: 14 KB per workgroup keeps the trace kernels
 // VGPR-limited rather than LDS-limited (deeper entries spill, see pt_device.h).
 #ifndef PT_WF_STACK
-#define PT_WF_STACK 16
+#define PT_WF_STACK 14
 #endif
 constexpr int kStack = PT_WF_STACK;
-// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 41 =
-// the three top levels (21) and 20 of the fourth, 5.1 KB).  With the 16-KB stack and the 10-KB
-// triangle batches (below) a workgroup takes 31.6 KB, so a CU still holds the 5 workgroups its
-// VGPRs allow.  Sweeps: 85 nodes without the batches and 21 / 41 / 85 before them were within
-// ±1 %; with them 41 beats 21 by 0.9 % and 5 loses 1 %.
+// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 57 =
+// the three top levels (21) and 36 of the fourth, 7.1 KB).  With the 14-KB stack and the 10-KB
+// triangle batches (below) a workgroup takes 31.7 KB, so a CU still holds the 5 workgroups its
+// VGPRs allow.  Sweeps on the v34 tree: 0 / 21 / 41 / 85 nodes with a 16-entry
+// stack -8.6 / -1.2 / 0 / -7.5 % Lambert (85: LDS-limited); 57 nodes with 14 stack entries
+// +1.2 %, 73 with 12 +0.5 %.
 #ifndef PT_LDS_NODES
-#define PT_LDS_NODES 41
+#define PT_LDS_NODES 57
 #endif
 constexpr int kLdsNodes = PT_LDS_NODES;
 // wave-batched triangle tests (pt_device.h wave_tri_batch): 2.5 KB of LDS per wave
