@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Copy a tools/round.sh TAG run from gpurun_out/ into profiles/ and refresh the derived files.
+
+    python tools/store_round.py TAG
+Copies the bench JSONs of every config, the GPU-test log, the rocprofv3 kernel stats (two-stream
+and one-stream passes) and the PMC traces; writes profiles/traffic.json and profiles/shade_pmc.json
+(tools/shade_pmc.py over the one-stream kernel stats).
+"""
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def main():
+    tag = sys.argv[1]
+    prof, rnd, out = ROOT / "gpurun_out" / f"prof_{tag}", ROOT / "gpurun_out" / f"round_{tag}", ROOT / "profiles"
+    cp = [(prof / "kt" / "run_kernel_stats.csv", f"{tag}_wavefront_kernel_stats.csv"),
+          (prof / "kt1" / "run_kernel_stats.csv", f"{tag}_wavefront_kernel_stats_single_stream.csv"),
+          (prof / "fetch" / "run_counter_collection.csv", f"{tag}_wavefront_pmc_fetch_trace.csv"),
+          (prof / "write" / "run_counter_collection.csv", f"{tag}_wavefront_pmc_write_trace.csv"),
+          (prof / "traffic.json", f"{tag}_wavefront_traffic.json"),
+          (prof / "traffic.json", "traffic.json"),
+          (rnd / "gputest.log", f"{tag}_gputest.log")]
+    cp += [(rnd / f"bench_config{c}.json", f"{tag}_bench_config{c}.json") for c in ("2", "3", "4l", "5", "4d")]
+    for src, dst in cp:
+        shutil.copyfile(src, out / dst)
+    pmc = subprocess.run([sys.executable, str(ROOT / "tools" / "shade_pmc.py"),
+                          str(out / f"{tag}_wavefront_pmc_fetch_trace.csv"), str(out / f"{tag}_wavefront_pmc_write_trace.csv"),
+                          str(out / f"{tag}_wavefront_kernel_stats_single_stream.csv")],
+                         check=True, capture_output=True, text=True).stdout
+    (out / "shade_pmc.json").write_text(pmc)
+
+
+if __name__ == "__main__":
+    main()
