@@ -22,7 +22,7 @@ extern "C" {
 #define PT_ERR_INVALID (-1)
 #define PT_ERR_HIP (-2)
 #define PT_ERR_STATE (-3)
-#define PT_ERR_NOMEM (-4)
+#define PT_ERR_NOMEM (-4) /* a device allocation failed with hipErrorOutOfMemory (queues, frame or scene buffers) */
 
 /* Material mode = which BSDF pair the closest-hit program uses.  The reference selects it
  * by (un)commenting lines in Renderer/OptiX/devicePrograms.cu:303-341. */

@@ -28,9 +28,11 @@ int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
 }
+// Device allocations that fail for lack of memory report PT_ERR_NOMEM (the caller can retry
+// with fewer frames per launch); every other HIP failure is PT_ERR_HIP.
 int hip_fail(hipError_t e, const char* where) {
     g_last_error = std::string(where) + ": " + hipGetErrorString(e);
-    return PT_ERR_HIP;
+    return e == hipErrorOutOfMemory ? PT_ERR_NOMEM : PT_ERR_HIP;
 }
 
 #define PT_HIP(call, where)                              \
