@@ -140,6 +140,21 @@ constexpr int kWavesSh = kBlockSh / 64;
 #define PT_SHF_WAVES_OTHER 1
 #endif
 constexpr int shf_waves(int mode) { return (mode == 1 || mode == 3) /*Lambert, Dielectric*/ ? PT_SHF_WAVES : PT_SHF_WAVES_OTHER; }
+// k_shade_fused / k_shade0_pixel block size per mode.  Conductor and Dielectric run in 256-thread
+// blocks: +12.6 % and +6.1 % with the two wavefront streams; Lambert loses 5 % at
+// 256, so it keeps 1024.
+#ifndef PT_SHF_BLOCK_DIELECTRIC
+#define PT_SHF_BLOCK_DIELECTRIC 256
+#endif
+#ifndef PT_SHF_BLOCK_CONDUCTOR
+#define PT_SHF_BLOCK_CONDUCTOR 256
+#endif
+#ifndef PT_SHF_BLOCK_LAMBERT
+#define PT_SHF_BLOCK_LAMBERT 1024
+#endif
+constexpr int shf_block(int mode) {
+    return mode == 3 ? PT_SHF_BLOCK_DIELECTRIC : mode == 2 ? PT_SHF_BLOCK_CONDUCTOR : PT_SHF_BLOCK_LAMBERT;
+}
 // k_shade_nee / k_shade_smp (Default / Layered: the stochastic GlossyDiffuse eval, the sample)
 // run in 256-thread blocks at 4 waves per SIMD (128 VGPRs).  (Round 2 before the bucketed
 // queues: one kernel with both phases behind a block barrier, where 256-thread blocks beat
@@ -471,21 +486,22 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
 // ray (queue 0 is in path order) -- so it is derived here instead of read, and every path's
 // radiance is written rather than updated.
 template <int MODE, bool TEX, bool SHADE0>
-__global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+__global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fused(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     constexpr bool shade0 = SHADE0;
     // Lambert (memory-bound, 56 VGPRs): the throughput in queue order (queue_beta), +1.6 %; the
     // Conductor and Dielectric kernels are register-bound, and holding it across the appends
     // cost them 1-2 %, so they gather it by path
     constexpr bool kBetaQ = MODE == kModeLambert;
     constexpr bool kShareOrigin = MODE == kModeLambert;
+    constexpr int kBlock = shf_block(MODE), kWaves = kBlock / 64;
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
-    __shared__ int lds_sh[kWavesSh + 1], lds_q[kWavesSh + 1];
-    if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
+    __shared__ int lds_sh[kWaves + 1], lds_q[kWaves + 1];
+    if ((int)(blockIdx.x * kBlock) >= n) return;  // block-uniform
     {
-        const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+        const int i = (int)(blockIdx.x * kBlock + threadIdx.x);
         const bool valid = i < n;
         bool emit_shadow = false, emit_next = false;
         f3 so, sdir, contrib, o, d, beta;
@@ -556,13 +572,13 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
             }
         }
         if (shade0 && valid) W.L[path] = l0;  // every path of the batch, hit or miss
-        const int qi = block_append(cnt(W, b + 1, kQueue), emit_next, lds_q);
+        const int qi = block_append<kWaves>(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
             if (kBetaQ) stqs(queue_beta(W, b + 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
         }
-        const int si = block_append(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
+        const int si = block_append<kWaves>(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
         if (emit_shadow) {
             // Lambert: a sampled direction is never below the surface (lambert_sample forces z >= 0),
             // so the continuation ray starts at the shadow ray's origin (sf.pos + 1e-3 * Ng, the
@@ -582,12 +598,13 @@ __global__ __launch_bounds__(kBlockSh, shf_waves(MODE)) void k_shade_fused(DevSc
 // wrote one hit record per pixel).  Per path: the operations of k_shade_fused<SHADE0> (throughput
 // 1, seed tea16(pixel, frame), radiance written, continuation appended to queue 1).
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockSh, 1) void k_shade0_pixel(DevScene S, DevLaunch L, WFState W, int nf) {
+__global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S, DevLaunch L, WFState W, int nf) {
     constexpr bool kBetaQ = MODE == kModeLambert;  // as k_shade_fused
+    constexpr int kBlock = shf_block(MODE), kWaves = kBlock / 64;
     const int P1 = L.width * L.height;
-    __shared__ int lds_q[kWavesSh + 1];
-    if ((int)(blockIdx.x * kBlockSh) >= P1) return;  // block-uniform
-    const int p = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+    __shared__ int lds_q[kWaves + 1];
+    if ((int)(blockIdx.x * kBlock) >= P1) return;  // block-uniform
+    const int p = (int)(blockIdx.x * kBlock + threadIdx.x);
     const bool valid = p < P1;
     int tri = -1;
     SurfaceHit sf;
@@ -636,7 +653,7 @@ __global__ __launch_bounds__(kBlockSh, 1) void k_shade0_pixel(DevScene S, DevLau
             }
         }
         if (valid) stqs(W.L + path, l0);  // every path of the batch, hit or miss
-        const int qi = block_append(cnt(W, 1, kQueue), emit_next, lds_q);
+        const int qi = block_append<kWaves>(cnt(W, 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
@@ -1027,10 +1044,10 @@ hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, con
         if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
         {
             if (shade0)
-                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, true>), item_grid(items, kBlockSh), dim3(kBlockSh), 0,
+                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, true>), item_grid(items, shf_block(MODE)), dim3(shf_block(MODE)), 0,
                                    stream, S, L, W, b, vis0);
             else
-                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, false>), item_grid(items, kBlockSh), dim3(kBlockSh), 0,
+                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, false>), item_grid(items, shf_block(MODE)), dim3(shf_block(MODE)), 0,
                                    stream, S, L, W, b, vis0);
         }
     } else if (phase == 0) {
@@ -1055,11 +1072,12 @@ hipError_t launch_shade(bool fused, const DevScene& S, const DevLaunch& L, const
 
 template <int MODE>
 hipError_t launch_shade0_pixel_t(const DevScene& S, const DevLaunch& L, const WFState& W, int nf, hipStream_t stream) {
-    const dim3 grid = item_grid(L.width * L.height, kBlockSh);
+    constexpr int block = shf_block(MODE);
+    const dim3 grid = item_grid(L.width * L.height, block);
     if (S.texinfo)
-        hipLaunchKernelGGL((k_shade0_pixel<MODE, true>), grid, dim3(kBlockSh), 0, stream, S, L, W, nf);
+        hipLaunchKernelGGL((k_shade0_pixel<MODE, true>), grid, dim3(block), 0, stream, S, L, W, nf);
     else
-        hipLaunchKernelGGL((k_shade0_pixel<MODE, false>), grid, dim3(kBlockSh), 0, stream, S, L, W, nf);
+        hipLaunchKernelGGL((k_shade0_pixel<MODE, false>), grid, dim3(block), 0, stream, S, L, W, nf);
     return hipGetLastError();
 }
 hipError_t launch_shade0_pixel(int mode, const DevScene& S, const DevLaunch& L, const WFState& W, int nf,
