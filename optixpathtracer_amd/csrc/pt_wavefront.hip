@@ -128,6 +128,10 @@ inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * k
 // starves waves.)
 constexpr int kBlockSh = 1024;
 constexpr int kWavesSh = kBlockSh / 64;
+#ifndef PT_SHA_BLOCK
+#define PT_SHA_BLOCK 1024  // k_shade_a (Default / Layered); 512 / 256: +0.7 % / -3 %, DESIGN.md §5
+#endif
+constexpr int kBlockShA = PT_SHA_BLOCK, kWavesShA = kBlockShA / 64;
 // k_shade_fused waves per SIMD: a CU holds two 1024-thread blocks only at <= 64 VGPRs (8 waves
 // per SIMD); at 65..128 VGPRs one block per CU halves the occupancy (measured: 66 VGPRs made
 // the Lambert shade 37 % slower).  Lambert fits 64 VGPRs untextured; Dielectric spills ~22
@@ -170,7 +174,7 @@ constexpr int kBlockShB = PT_SHB_BLOCK;
 // Block-wide compaction: every thread of the block calls this (uniform control flow);
 // threads with pred get consecutive slots.  `lds` is kWavesSh + 1 ints of shared memory
 // private to this call site.
-template <int WAVES = kWavesSh>
+template <int WAVES>
 __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     const unsigned long long m = __ballot(pred ? 1 : 0);
     const int prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -733,13 +737,13 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
 // and either a shadow ray (visibility still unknown; the ray carries item | bucket << 28) or,
 // at bounce 0 with the (pixel, light) visibility table, the NEE queue directly.
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
+__global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, WFState W, int b, int vis0) {
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
-    __shared__ int lds_sh[kWavesSh + 1];
-    __shared__ int lds_nee[kShadeBuckets * (kWavesSh + 1)], lds_smp[kShadeBuckets * (kWavesSh + 1)];
-    if ((int)(blockIdx.x * kBlockSh) >= n) return;  // block-uniform
-    const int i = (int)(blockIdx.x * kBlockSh + threadIdx.x);
+    __shared__ int lds_sh[kWavesShA + 1];
+    __shared__ int lds_nee[kShadeBuckets * (kWavesShA + 1)], lds_smp[kShadeBuckets * (kWavesShA + 1)];
+    if ((int)(blockIdx.x * kBlockShA) >= n) return;  // block-uniform
+    const int i = (int)(blockIdx.x * kBlockShA + threadIdx.x);
     bool emit = false;
     int nee_bucket = -1, smp_bucket = -1, code = 0;
     f3 so, sdir;
@@ -782,14 +786,14 @@ __global__ __launch_bounds__(kBlockSh) void k_shade_a(DevScene S, DevLaunch L, W
             }
         }
     }
-    const int si = block_append(cnt(W, b, kShadowQ), emit, lds_sh);
+    const int si = block_append<kWavesShA>(cnt(W, b, kShadowQ), emit, lds_sh);
     if (emit) {
         W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(code));
         W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
     }
-    const int ni = block_append_k<kWavesSh, kShadeBuckets>(cnt(W, b, kNee0), nee_bucket, lds_nee);
+    const int ni = block_append_k<kWavesShA, kShadeBuckets>(cnt(W, b, kNee0), nee_bucket, lds_nee);
     if (nee_bucket >= 0) W.nq[(size_t)nee_bucket * W.paths + ni] = i;
-    const int mi = block_append_k<kWavesSh, kShadeBuckets>(cnt(W, b, kSmp0), smp_bucket, lds_smp);
+    const int mi = block_append_k<kWavesShA, kShadeBuckets>(cnt(W, b, kSmp0), smp_bucket, lds_smp);
     if (smp_bucket >= 0) W.sq[(size_t)smp_bucket * W.paths + mi] = i;
 }
 
@@ -1051,7 +1055,7 @@ hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, con
                                    stream, S, L, W, b, vis0);
         }
     } else if (phase == 0) {
-        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockSh), dim3(kBlockSh), 0, stream, S, L, W, b,
+        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockShA), dim3(kBlockShA), 0, stream, S, L, W, b,
                            vis0);
     } else if (phase == 1) {
         hipLaunchKernelGGL((k_shade_nee<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L,
