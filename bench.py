@@ -7,14 +7,15 @@
 
 Workload (configs[1]): the synthetic Diffuse sphere-in-box scene (34,570 triangles,
 Lambert mode, Scene1 camera and 4 point lights), 1920x1080, depth 8.  One STEP = one
-1024-spp render of the full frame per GPU: every rank renders its own disjoint frame-id
-range (spp sharding) into a device fp32 accumulator, then the
-accumulators are summed to rank 0 with one RCCL reduce (torch.distributed "nccl" = RCCL
-over xGMI).  Per-GPU work is fixed as N grows ("weak" scaling); value = all samples of
-all ranks / max-over-ranks wall time.
+1024-spp render of the full frame: the 1024 frame ids are split over the ranks (spp
+sharding), every rank renders its share into a device fp32 accumulator, and
+the accumulators are summed to rank 0 with one RCCL reduce (torch.distributed "nccl" = RCCL
+over xGMI).  The image is fixed as N grows ("strong" scaling, north_star's 1 -> 8 GPU scaling
+of the 1024-spp image); value = the step's samples / max-over-ranks wall time.  At N > 1 one
+more step with 1024 frames per rank reports the weak-scaling rate as `value_weak`.
 
-`--config 3|4d|4l|5` runs BASELINE.json's other configs through the same harness (4d/4l split
-4096 spp over the ranks: strong scaling); the driver's default run is configs[1].
+`--config 3|4d|4l|5` runs BASELINE.json's other configs through the same harness (4d/4l: 4096
+spp per step); the driver's default run is configs[1].
 
 Extra fields: `roofline` (HBM roofline of the dominant kernels, the wavefront's trace kernels
 k_extend + k_trace_pair: 48 algorithmic bytes per traced ray, ray read + result write, over
@@ -45,22 +46,34 @@ BYTES_PER_TRACE = 48  # trace-kernel share per ray: ray record read 32 B + hit /
 # BASELINE.json configs by index: scene, spp per step, scaling, workload label.  The default
 # (configs[1]) is the headline; the others are reported in DESIGN.md from the same harness.
 CONFIGS = {
-    "2": ("sphere_box_diffuse", 1024, "weak",
+    "2": ("sphere_box_diffuse", 1024, "strong",
           "BASELINE configs[1]: Diffuse sphere-in-box 1920x1080, 1024 spp, depth 8"),
-    "3": ("sphere_box_conductor", 1024, "weak",
+    "3": ("sphere_box_conductor", 1024, "strong",
           "BASELINE configs[2]: Conductor (Trowbridge-Reitz) spheres + Layered walls (Default mode), "
           "1920x1080, 1024 spp, depth 8"),
     "4d": ("sphere_box_dielectric20", 4096, "strong",
            "BASELINE configs[3] (i): Dielectric-bright 1920x1080, 4096 spp split over the GPUs + RCCL reduce"),
     "4l": ("sphere_box_layered", 4096, "strong",
            "BASELINE configs[3] (ii): Layered 1920x1080, 4096 spp split over the GPUs + RCCL reduce"),
-    "5": ("sponza_class", 1024, "weak",
+    "5": ("sponza_class", 1024, "strong",
           "BASELINE configs[4]: Sponza-class procedural atrium (~250k tris, mixed BRDFs) 1920x1080, 1024 spp"),
 }
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def pmc_record(path: Path, sources_sha: str):
+    """A committed PMC summary (profiles/*.json) and whether it belongs to these kernel sources.
+    Returns (data, current): figures measured on other sources are never reported as this tree's."""
+    if not path.exists():
+        return None, False
+    try:
+        d = json.loads(path.read_text())
+    except Exception:
+        return None, False
+    return d, d.get("sources_sha") == sources_sha
 
 
 def parse():
@@ -87,8 +100,11 @@ def parse():
     ap.add_argument("--wavefront-streams", type=int, default=2,
                     help="streams the wavefront batches alternate between (pt_set_wavefront_streams)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
-                    help="override the config's scaling: strong = the step's spp in total, split over the "
-                         "ranks (for configs[1]: the one 1024-spp headline image rendered by N GPUs)")
+                    help="override the config's scaling (all configs: strong = the step's spp in total, split "
+                         "over the ranks; weak = the step's spp per rank)")
+    ap.add_argument("--reference-loops", type=int, default=64,
+                    help="pt_render calls (1 spp each, frame.id++, 24.9 MB download per call: the reference's "
+                         "OptixView::DrawOptix -> OptixRenderer::Render loop) timed for value_reference_loop; 0 = off")
     a = ap.parse_args()
     scene, spp, scaling, a.workload = CONFIGS[a.config]
     a.scaling = a.scaling or scaling
@@ -168,18 +184,14 @@ def main():
 
     from optixpathtracer_amd import sharding
 
-    def step(s: int):
-        r.accum_clear()
-        if args.scaling == "strong":  # args.spp frames per step in total, split over the ranks
+    def step(s: int, scaling: str | None = None):
+        if (scaling or args.scaling) == "strong":  # args.spp frames per step in total, split over the ranks
             first, n = sharding.split_frames(args.spp, rank, world, base=1 + s * args.spp)
         else:  # args.spp frames per rank per step; disjoint frame ids per (step, rank)
             first, n = sharding.frame_range(s, rank, world, args.spp)
-        r.render_frames(first, n)
-        r.synchronize()
-        sharding.reduce_accumulator(accum, dist)  # RCCL over xGMI
-        # the reduce runs on torch's stream, the next step's clear and render on libptamd's:
-        # finish the reduce before this step ends, so the next clear cannot overtake it
-        torch.cuda.current_stream(dev).synchronize()
+        # clear -> render -> sync -> RCCL reduce over xGMI -> sync torch's stream (the next
+        # step's clear runs on libptamd's stream and must not overtake the reduce)
+        sharding.render_step(r, accum, dist, first, n)
 
     for s in range(args.warmup):
         step(s)
@@ -229,6 +241,22 @@ def main():
             e1 = float(t.item())
         value_nodedup = args.width * args.height * per_step_spp / e1 / 1e6
         r.set_primary_dedup(True)
+    # Transparency at N > 1: the other scaling mode's rate from one more step (weak: every rank
+    # renders the step's full spp; strong: the ranks split it)
+    value_other = None
+    if world > 1:
+        other = "weak" if args.scaling == "strong" else "strong"
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        step(args.warmup + args.steps + 2, scaling=other)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        e3 = time.perf_counter() - t3
+        t = torch.tensor([e3], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        e3 = float(t.item())
+        value_other = (other, args.width * args.height * (args.spp * world if other == "weak" else args.spp) / e3 / 1e6)
     # Transparency: the timed steps alternate the wavefront batches between two streams
     # (pt_set_wavefront_streams, default 2), so a trace launch shares the GPU with the other
     # batch's kernels and its event window is longer than its solo run.  One more step on a
@@ -276,34 +304,41 @@ def main():
             avg_launch_s = kernel_s / launches
             bytes_def = "396 B per segment + 12 B per sample"
         achieved = per_launch_bytes / avg_launch_s / 1e9
+        # PMC figures come from separate rocprofv3 passes committed under profiles/ (tools/profile.sh,
+        # tools/pmc.sh); each carries the kernel-source hash it was measured on.  Only figures of
+        # these sources fill the contract fields; older ones are listed under pmc_stale.
+        from optixpathtracer_amd.provenance import kernel_sources_sha
+        sha = kernel_sources_sha()
+        pmc_stale = {}
         traffic = traffic_low = None
-        tj = Path(args.traffic_json)
-        if tj.exists():
-            try:
-                tjd = json.loads(tj.read_text())
-                if tjd.get("kernel") == dom and tjd.get("config", "2") == args.config:
-                    traffic = tjd.get("hbm_bytes_per_launch")
-                    traffic_low = tjd.get("hbm_bytes_per_launch_low")
-            except Exception:
-                traffic = traffic_low = None
+        tjd, cur = pmc_record(Path(args.traffic_json), sha)
+        if tjd and tjd.get("kernel") == dom and tjd.get("config", "2") == args.config:
+            fig = {"hbm_bytes_per_launch": tjd.get("hbm_bytes_per_launch"),
+                   "hbm_bytes_per_launch_low": tjd.get("hbm_bytes_per_launch_low")}
+            if cur:
+                traffic, traffic_low = fig["hbm_bytes_per_launch"], fig["hbm_bytes_per_launch_low"]
+            else:
+                pmc_stale["traffic"] = {**fig, "sources_sha": tjd.get("sources_sha"), "stale": True}
         valu = None  # the VALU fraction beside the HBM roofline, from PMC passes
-        vj = ROOT / "profiles" / "valu.json"
-        if vj.exists() and dom == "k_extend+k_trace_pair" and args.config == "2":
-            try:
-                vd = json.loads(vj.read_text())
-                valu = {k: vd[k] for k in ("kernel", "valu_busy", "lane_utilisation")}
-            except Exception:
-                valu = None
+        vd, cur = pmc_record(ROOT / "profiles" / "valu.json", sha)
+        if vd and dom == "k_extend+k_trace_pair" and args.config == "2":
+            fig = {k: vd.get(k) for k in ("kernel", "valu_busy", "lane_utilisation")}
+            if cur:
+                valu = {**fig, "sources_sha": sha}
+            else:
+                pmc_stale["valu_pmc"] = {**fig, "sources_sha": vd.get("sources_sha"), "stale": True}
         shade = None  # the memory-bound kernel of a Lambert frame, PMC HBM GB/s (tools/shade_pmc.py)
-        sj = ROOT / "profiles" / "shade_pmc.json"
-        if sj.exists() and dom == "k_extend+k_trace_pair" and args.config == "2":
-            try:
-                ks = json.loads(sj.read_text())["kernels"]
-                # bounces >= 1 (the bounce-0 instance derives its path state, shade0)
-                sk = ks.get("k_shade_fused<1, false, false>") or ks["k_shade_fused<1, false>"]
-                shade = {"kernel": "k_shade_fused<Lambert>", **{k: sk[k] for k in ("hbm_gbps", "frac", "avg_launch_ms")}}
-            except Exception:
-                shade = None
+        sd, cur = pmc_record(ROOT / "profiles" / "shade_pmc.json", sha)
+        if sd and dom == "k_extend+k_trace_pair" and args.config == "2":
+            ks = sd.get("kernels", {})
+            # bounces >= 1 (the bounce-0 instance derives its path state, shade0)
+            sk = ks.get("k_shade_fused<1, false, false>") or ks.get("k_shade_fused<1, false>")
+            if sk:
+                fig = {"kernel": "k_shade_fused<Lambert>", **{k: sk[k] for k in ("hbm_gbps", "frac", "avg_launch_ms")}}
+                if cur:
+                    shade = {**fig, "sources_sha": sha}
+                else:
+                    pmc_stale["shade_pmc"] = {**fig, "sources_sha": sd.get("sources_sha"), "stale": True}
         out = {
             "metric": "Msamples/sec at 1920x1080, max-depth 8; MSE vs reference",
             "value": round(value, 3),
@@ -338,6 +373,8 @@ def main():
             # one extra step with pt_set_primary_dedup(0): each frame traces its own copy of the
             # (identical, unjittered) camera rays; same image bit for bit
             "value_primary_per_frame": None if value_nodedup is None else round(value_nodedup, 3),
+            # N > 1: the other scaling mode's rate from one extra step (value_weak / value_strong)
+            **({f"value_{value_other[0]}": round(value_other[1], 3)} if value_other else {}),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
@@ -359,17 +396,45 @@ def main():
                 # PMC HBM bandwidth of the shading kernel (2 x FETCH_SIZE + WRITE_SIZE per launch)
                 "shade_pmc": shade,
                 "single_stream": single,
+                # the kernel sources of this run; PMC figures measured on other sources (never
+                # reported in the fields above)
+                "sources_sha": sha,
+                "pmc_stale": pmc_stale or None,
             },
             "image": {"mean": float(np.nanmean(img) / per_step_spp), "nan_pixels": nan_px},
         }
+        if world == 1 and args.reference_loops > 0 and args.kernel != 0:
+            # The reference's own call pattern (OptixView::DrawOptix -> OptixRenderer::Render,
+            # OptixView.cpp:201-210, OptixRenderer.cpp:617-647): one pt_render per spp (frame.id++,
+            # one 1-frame wavefront batch) and a download of the 24.9 MB frame into a freshly
+            # allocated host array every call; the GL upload and blend are not part of it.
+            fid = r.frame_id
+            r.frame_id = 0
+            r.Render()  # first call sizes the 1-frame queues
+            t4 = time.perf_counter()
+            for _ in range(args.reference_loops):
+                r.Render(np.empty((args.height, args.width, 3), np.float32))
+            e4 = time.perf_counter() - t4
+            r.frame_id = fid
+            out["value_reference_loop"] = round(args.width * args.height * args.reference_loops / e4 / 1e6, 3)
+            out["reference_loop"] = {"calls": args.reference_loops, "ms_per_call": round(e4 / args.reference_loops * 1e3, 3),
+                                     "what": "pt_render: 1 spp per call, frame.id++, D2H download of the 24.9 MB "
+                                             "frame per call (the reference's DrawOptix loop)"}
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline (oracle) ...")
             band, spp_cpu, out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_baseline_seconds)
             # "MSE vs reference" of the metric: the GPU renders the same frame ids (1..spp_cpu)
-            # untimed, and its band is compared with the oracle's per-pixel mean radiance
+            # untimed, and its band is compared with the oracle's per-pixel mean radiance.  The
+            # render runs the timed configuration's machinery: batches of a third of the frames
+            # (so at least two batches, alternating over the wavefront streams, and a ragged tail
+            # when spp_cpu is not a multiple of three).
+            fpl_check = max(1, -(-spp_cpu // 3))
+            r.set_frames_per_launch(fpl_check)
             r.accum_clear()
             r.render_frames(1, spp_cpu)
             r.synchronize()
+            r.set_frames_per_launch(args.frames_per_launch)
+            n_batches = -(-spp_cpu // fpl_check)
             gpu = accum.cpu().numpy()[args.height - band.shape[0]:].astype(np.float64) / spp_cpu
             ref = band.astype(np.float64) / spp_cpu
             diff = np.nan_to_num(gpu, nan=0.0) - np.nan_to_num(ref, nan=0.0)  # NaN -> 0 (WriteImage.cpp:52-55)
@@ -380,6 +445,9 @@ def main():
                 "max_abs": float(np.max(np.abs(diff))),
                 "bar": 1e-5,
                 "sample": out["cpu_baseline"]["sample"].split(",")[0] + " (GPU render of the same frame ids)",
+                "gpu_batches": n_batches,
+                "gpu_frames_per_batch": fpl_check,
+                "gpu_streams": min(n_batches, args.wavefront_streams),
             }
         print(json.dumps(out), flush=True)
     r.close()

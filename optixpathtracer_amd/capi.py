@@ -16,6 +16,7 @@ LIB_PATH = _HERE / "libptamd.so"
 PT_MAT_DEFAULT, PT_MAT_LAMBERT, PT_MAT_CONDUCTOR, PT_MAT_DIELECTRIC, PT_MAT_LAYERED = range(5)
 PT_KERNEL_MEGA, PT_KERNEL_WAVEFRONT, PT_KERNEL_AUTO = 0, 1, 2
 PT_BVH_PLOC, PT_BVH_LBVH = 0, 1
+PT_OK, PT_ERR_INVALID, PT_ERR_HIP, PT_ERR_STATE, PT_ERR_NOMEM = 0, -1, -2, -3, -4
 
 MATERIAL_MODES = {
     "default": PT_MAT_DEFAULT,
@@ -27,7 +28,11 @@ MATERIAL_MODES = {
 
 
 class PTError(RuntimeError):
-    """A libptamd call returned a negative status."""
+    """A libptamd call returned a negative status (`status`: PT_ERR_*)."""
+
+    def __init__(self, msg: str, status: int = 0):
+        super().__init__(msg)
+        self.status = status
 
 
 class pt_mesh(C.Structure):
@@ -236,7 +241,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
 def check(status: int, what: str = "") -> None:
     if status != 0:
         msg = load().pt_last_error()
-        raise PTError(f"{what} failed ({status}): {msg.decode() if msg else ''}")
+        raise PTError(f"{what} failed ({status}): {msg.decode() if msg else ''}", status)
 
 
 def fptr(a):

@@ -89,7 +89,11 @@ struct EventPool {
 // overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces
 // [9..13] wave schedule of the trace kernels (pt_stats wave_*).
 constexpr int kCounters = 16;
-constexpr int kMinTraversalStack = 14 + kSpillDepth;  // pt_wavefront.hip kStack + pt_device.h kSpillDepth
+// event pairs held by one renderer before launch_frames retires them (EventPool)
+constexpr size_t kMaxPendingEvents = 4096;
+// the smallest traversal stack of any kernel (pt_device.h stack_capacity: 77 entries for the
+// wavefront's 14 LDS entries and 64 spill slots in chunks of 7)
+constexpr int kMinTraversalStack = std::min(stack_capacity(PT_WF_STACK), stack_capacity(PT_MK_STACK));
 
 }  // namespace
 
@@ -236,6 +240,10 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
 // are summed at the next pt_synchronize / pt_get_stats / download (collect_pending).
 int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, double* accum64 = nullptr) {
     int rc = PT_OK;
+    // callers that never synchronise through the library (pt_stream interop, device sum buffers,
+    // loops over pt_launch / pt_display_add_frame) would grow the event pools without bound:
+    // past kMaxPendingEvents pairs, retire them first (this waits for the enqueued work)
+    if (r->ev.used + r->tev.used > kMaxPendingEvents && (rc = collect_pending(r)) != PT_OK) return rc;
     const DevScene S = r->scene();
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
@@ -260,17 +268,24 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // VALU-bound tracing of the other, and each kernel's SIMT tail filled); k_accum still adds
         // the batches in frame order (accum_wait / accum_done)
         const int nbatch = (int)((n + (uint32_t)nf_cap - 1) / (uint32_t)nf_cap);
-        const int ns = std::max(1, std::min(r->wf_streams, nbatch));
-        const bool dual = ns > 1;
+        int ns = std::max(1, std::min(r->wf_streams, nbatch));
         for (int k = 0; k < ns; ++k) {
             WFState& w = k ? r->xwf[k] : r->wf;
             if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces) {
                 for (int j = 0; j < pt_renderer::kMaxWFStreams; ++j)
                     if (r->wf_stream(j)) PT_HIP(hipStreamSynchronize(r->wf_stream(j)), "hipStreamSynchronize");
                 wavefront_free(w);
-                PT_HIP(wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces)), "wavefront_alloc");
+                const hipError_t ae = wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces));
+                // the extra streams only overlap batches: when their queues do not fit, render on
+                // the k streams that do (the image is the same, added in frame order either way)
+                if (ae == hipErrorOutOfMemory && k > 0) {
+                    ns = k;
+                    break;
+                }
+                PT_HIP(ae, "wavefront_alloc");
             }
         }
+        const bool dual = ns > 1;
         if (dual && !r->ev_fork) {
             PT_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming), "hipEventCreate");
             for (hipEvent_t& e : r->ev_accum) PT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
@@ -611,7 +626,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         r->bvh_nodes = bo.n_nodes;
         r->bvh_depth = bo.depth;
         // a traversal holds at most 3 stack entries per BVH4 level; the smallest traversal stack
-        // (wavefront: 14 LDS + 64 spill entries) must hold them, or rays could lose subtrees
+        // (kMinTraversalStack) must hold them, or rays could lose subtrees
         if (3 * bo.depth > kMinTraversalStack)
             return cleanup_fail(fail(PT_ERR_INVALID, "pt_create: BVH too deep for the traversal stack (depth " +
                                                          std::to_string(bo.depth) + ")"));
@@ -958,9 +973,14 @@ int pt_set_accum_fp64(pt_renderer* r, int32_t on) {
         std::vector<double> h64(n);
         const float* src = r->comms.empty() ? r->accum() : r->d_part;
         double* dst = r->comms.empty() ? r->d_accum64 : r->d_part64;
-        PT_HIP(hipMemcpy(h32.data(), src, n * sizeof(float), hipMemcpyDeviceToHost), "download accum");
+        // on the library stream, after alloc_accum64's zeroing: a null-stream hipMemcpy would not
+        // wait for the non-blocking stream, and the memset could land on the seeded sum
+        PT_HIP(hipMemcpyAsync(h32.data(), src, n * sizeof(float), hipMemcpyDeviceToHost, r->stream), "download accum");
+        PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
         for (size_t i = 0; i < n; ++i) h64[i] = (double)h32[i];
-        PT_HIP(hipMemcpy(dst, h64.data(), n * sizeof(double), hipMemcpyHostToDevice), "upload fp64 accum");
+        PT_HIP(hipMemcpyAsync(dst, h64.data(), n * sizeof(double), hipMemcpyHostToDevice, r->stream),
+               "upload fp64 accum");
+        PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     } else if (!r->accum64) {
         if (r->d_accum64) (void)hipFree(r->d_accum64);
         if (r->d_part64) (void)hipFree(r->d_part64);

@@ -159,9 +159,21 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
 // slow flat load on every step).
 // The LDS depth is a template parameter (DEPTH): it trades LDS per workgroup against
 // occupancy per kernel (see pt_render.hip / pt_wavefront.hip).  A traversal holds at most
-// 3 entries per BVH4 level, so DEPTH + kSpillDepth must be >= 3 * depth; pt_create rejects
-// deeper trees (kMaxBvhDepth).
+// 3 entries per BVH4 level; pt_create rejects trees deeper than the smallest traversal
+// stack holds (stack_capacity).
 constexpr int kSpillDepth = 64;
+// LDS stack depths of the wavefront trace kernels and of the megakernel / k_trace (A/B builds
+// override them with -D; every translation unit sees the same value)
+#ifndef PT_WF_STACK
+#define PT_WF_STACK 14
+#endif
+#ifndef PT_MK_STACK
+#define PT_MK_STACK 32
+#endif
+// Entries a traversal with an LDS stack of `lds` entries holds without losing one: the spill
+// moves chunks of lds/2 entries, so only whole chunks of kSpillDepth are usable, and the LDS
+// part fills up to `lds` (a push of <= 3 happens at sp <= lds - 3).
+constexpr int stack_capacity(int lds) { return (kSpillDepth / (lds / 2)) * (lds / 2) + lds; }
 
 // ---- textures: devicePrograms.cu:62-73 (SRGB8ToLinear), :131-166 (GetTextureCoord,
 // SampleTextures), :518-543 (AlphaCutout); CreateTextures (OptixRenderer.cpp:562-612) sets up

@@ -15,10 +15,8 @@ namespace pt {
 namespace {
 
 constexpr int kBlock = 256;
-// LDS traversal stack entries per lane (the megakernel is VGPR-limited, not LDS-limited).
-#ifndef PT_MK_STACK
-#define PT_MK_STACK 32
-#endif
+// LDS traversal stack entries per lane (PT_MK_STACK, pt_device.h; the megakernel is
+// VGPR-limited, not LDS-limited).
 constexpr int kStack = PT_MK_STACK;
 // Minimum waves per SIMD the register allocator must allow (caps VGPRs at 512/N).
 #ifndef PT_MK_WAVES

@@ -38,11 +38,8 @@ namespace pt {
 namespace {
 
 constexpr int kBlockWF = 256;
-// LDS traversal stack entries per lane: 14 KB per workgroup keeps the trace kernels
-// VGPR-limited rather than LDS-limited (deeper entries spill, see pt_device.h).
-#ifndef PT_WF_STACK
-#define PT_WF_STACK 14
-#endif
+// LDS traversal stack entries per lane (PT_WF_STACK, pt_device.h): 14 KB per workgroup keeps
+// the trace kernels VGPR-limited rather than LDS-limited (deeper entries spill).
 constexpr int kStack = PT_WF_STACK;
 // Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 57 =
 // the three top levels (21) and 36 of the fourth, 7.1 KB).  With the 14-KB stack and the 10-KB
@@ -1141,6 +1138,13 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
     al((void**)&W.nq, P * kShadeBuckets * sizeof(int));
     al((void**)&W.sq, P * kShadeBuckets * sizeof(int));
     al((void**)&W.count, count_bytes(max_bounces));
+    if (e != hipSuccess) {
+        // no partial queue set survives a failed allocation: paths stays 0, so the next
+        // launch_frames allocates again instead of launching on null queues
+        wavefront_free(W);
+        (void)hipGetLastError();
+        return e;
+    }
     W.paths = paths;
     W.max_bounces = max_bounces;
     return e;

@@ -24,6 +24,31 @@ def split_frames(total_spp: int, rank: int, world: int, base: int = 1) -> tuple[
 
 
 def reduce_accumulator(tensor, dist, dst: int = 0) -> None:
-    """Sum every rank's accumulator into rank `dst` (one collective per image)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(tensor, dst=dst, op=dist.ReduceOp.SUM)
+    """Sum every rank's accumulator into rank `dst` (one collective per image).
+
+    With RCCL ("nccl") the device tensor is reduced in place over xGMI.  gloo (the CPU tests, or
+    several ranks sharing one GPU, where RCCL cannot run) reduces host tensors: a device
+    accumulator is then copied to the host, reduced, and copied back on rank `dst`."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() <= 1:
+        return
+    if tensor.is_cuda and dist.get_backend() == "gloo":
+        host = tensor.cpu()
+        dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM)
+        if dist.get_rank() == dst:
+            tensor.copy_(host)
+        return
+    dist.reduce(tensor, dst=dst, op=dist.ReduceOp.SUM)
+
+
+def render_step(renderer, accum, dist, first: int, n: int) -> None:
+    """One bench.py step on one rank: clear -> render frames first .. first+n-1 into the device
+    accumulator `accum` (a torch tensor registered with pt_set_accum_device_buffer) -> wait for
+    libptamd's stream -> reduce to rank 0 -> wait for torch's stream.  The reduce runs on torch's
+    stream and the next step's clear on libptamd's, so the step ends only after the reduce."""
+    import torch
+
+    renderer.accum_clear()
+    renderer.render_frames(first, n)
+    renderer.synchronize()
+    reduce_accumulator(accum, dist)
+    torch.cuda.current_stream(accum.device).synchronize()

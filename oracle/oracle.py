@@ -268,7 +268,8 @@ class OracleScene:
             sum_rgb = np.zeros((h, w, 3), np.float32)
         x0, y0, x1, y1 = rect if rect is not None else (0, 0, w, h)
         segs = C.c_uint64()
-        nt = threads or os.cpu_count() or 1
+        # the host's CPU share: OMP_NUM_THREADS where the box sets it (16 per GPU), else all cores
+        nt = threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count() or 1
         self.lib.orc_render(self.h, C.byref(lp), int(first_frame), int(n_frames), x0, y0, x1, y1, fp(sum_rgb), nt,
                             C.byref(segs))
         return sum_rgb, int(segs.value)

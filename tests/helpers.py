@@ -13,8 +13,10 @@ def image_mse(a: np.ndarray, b: np.ndarray) -> float:
     return float(np.mean((a - b) ** 2))
 
 
-def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, kernel=0, device=0,
-               frames_per_launch=None):
+def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, kernel=2, device=0,
+               frames_per_launch=None, streams=None, kernel_timing=False):
+    """Render through the C ABI.  kernel 2 (PT_KERNEL_AUTO, the default) is the product path
+    bench.py times: the wavefront with 64-frame batches alternating over two streams."""
     from optixpathtracer_amd.renderer import setup_renderer
 
     r = setup_renderer(scene, width, height, max_bounces, device=device, kernel=kernel)
@@ -22,6 +24,10 @@ def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=No
         r.set_material_mode(mode)
     if frames_per_launch is not None:
         r.set_frames_per_launch(frames_per_launch)
+    if streams is not None:
+        r.set_wavefront_streams(streams)
+    if kernel_timing:
+        r.set_kernel_timing(True)
     r.accum_clear()
     r.render_frames(first_frame, n_frames)
     img = r.accum()

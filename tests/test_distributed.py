@@ -136,3 +136,66 @@ def test_two_process_gpu_shards_reduce_to_single_render(tmp_path):
     want = r.accum()
     r.close()
     np.testing.assert_allclose(got, want, rtol=2e-6, atol=1e-7)
+
+
+def _gpu_bench_worker(rank, world, port, spp, steps, out_dir):
+    """bench.py's per-rank loop with a device accumulator: per step, sharding.render_step (clear
+    -> render -> sync -> reduce -> sync); rank 0 keeps each step's reduced sum."""
+    sys.path.insert(0, str(ROOT))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from optixpathtracer_amd import scenes, sharding
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    # one GPU on the test box: RCCL needs a GPU per rank, so the collective runs over gloo on
+    # host copies (sharding.reduce_accumulator); buffers, streams and step order are bench.py's
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    sc = scenes.tiny_scene("conductor")
+    r = setup_renderer(sc, 48, 32, 5, device=0)
+    r.set_frames_per_launch(3)  # several batches over both wavefront streams per step
+    accum = torch.zeros((32, 48, 3), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)
+    r.set_accum_device_buffer(accum.data_ptr())
+    for s in range(steps):
+        first, n = sharding.split_frames(spp, rank, world, base=1 + s * spp)
+        sharding.render_step(r, accum, dist, first, n)
+        if rank == 0:
+            np.save(os.path.join(out_dir, f"step{s}.npy"), accum.cpu().numpy())
+    dist.barrier()
+    r.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_process_bench_steps_device_accumulators(tmp_path):
+    """Two ranks on one GPU run three bench-style steps (strong split of 11 frames per step) on
+    torch device accumulators.  Rank 0's sum after each step equals, bit for bit, the fp32 sum of
+    the two ranks' shards rendered separately (the reduce adds two fp32 images), and the shards
+    together hold every frame of the step: a clear overtaking the previous reduce, or a reduce
+    reading a half-rendered sum, changes these bits."""
+    import torch.multiprocessing as mp
+
+    from optixpathtracer_amd import scenes, sharding
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    world, spp, steps = 2, 11, 3
+    mp.spawn(_gpu_bench_worker, args=(world, _free_port(), spp, steps, str(tmp_path)), nprocs=world, join=True)
+    sc = scenes.tiny_scene("conductor")
+    r = setup_renderer(sc, 48, 32, 5, device=0)
+    for s in range(steps):
+        got = np.load(tmp_path / f"step{s}.npy")
+        shards = []
+        for rank in range(world):
+            first, n = sharding.split_frames(spp, rank, world, base=1 + s * spp)
+            r.accum_clear()
+            r.render_frames(first, n)
+            shards.append(r.accum())
+        np.testing.assert_array_equal(got, shards[0] + shards[1])
+        r.accum_clear()
+        r.render_frames(1 + s * spp, spp)
+        np.testing.assert_allclose(got, r.accum(), rtol=2e-6, atol=1e-7)
+    r.close()

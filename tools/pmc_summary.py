@@ -1,16 +1,32 @@
 #!/usr/bin/env python3
 """Summarise tools/pmc.sh output for one kernel: per-dispatch means and derived ratios.
 
-    python tools/pmc_summary.py OUTDIR KERNEL_SUBSTRING
+    python tools/pmc_summary.py OUTDIR KERNEL_SUBSTRING [--valu-json OUT --waves N --source TEXT]
+
+--valu-json writes the VALU figures bench.py reports as roofline.valu_pmc (profiles/valu.json),
+tagged with the kernel sources they were measured on; --waves is the kernel's waves per SIMD
+(SQ counters are per wave, so busy = issue fraction x resident waves).
 """
+import argparse
 import csv
+import json
 import sys
 from collections import defaultdict
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from optixpathtracer_amd.provenance import kernel_sources_sha  # noqa: E402
+
 
 def main():
-    root, kname = Path(sys.argv[1]), sys.argv[2]
+    ap = argparse.ArgumentParser()
+    ap.add_argument("outdir")
+    ap.add_argument("kernel")
+    ap.add_argument("--valu-json", default=None)
+    ap.add_argument("--waves", type=int, default=5)
+    ap.add_argument("--source", default="")
+    a = ap.parse_args()
+    root, kname = Path(a.outdir), a.kernel
     acc = defaultdict(list)
     for f in root.rglob("*counter_collection.csv"):
         for row in csv.DictReader(open(f)):
@@ -32,6 +48,18 @@ def main():
                 print(f"{k:24s} / VALU insts   {g(k) / g('SQ_INSTS_VALU'):.3f}")
     if g("TCC_HIT_sum") is not None and g("TCC_MISS_sum") is not None:
         print(f"L2 hit rate                {g('TCC_HIT_sum') / max(1.0, g('TCC_HIT_sum') + g('TCC_MISS_sum')):.4f}")
+    if a.valu_json and g("SQ_ACTIVE_INST_VALU") and g("SQ_WAVE_CYCLES") and g("SQ_THREAD_CYCLES_VALU"):
+        issue = g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES")
+        Path(a.valu_json).write_text(json.dumps({
+            "kernel": kname,
+            "source": a.source or f"tools/pmc.sh -> {root}",
+            "sources_sha": kernel_sources_sha(),
+            "waves_per_simd": a.waves,
+            "valu_issue_per_wave_cycle": round(issue, 3),
+            "valu_busy": round(min(1.0, issue * a.waves), 3),
+            "lane_utilisation": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 3),
+            "wait_per_wave_cycle": round(g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES"), 3) if g("SQ_WAIT_ANY") else None,
+        }, indent=1) + "\n")
 
 
 if __name__ == "__main__":

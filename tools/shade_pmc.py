@@ -14,6 +14,10 @@ import csv
 import json
 import re
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from optixpathtracer_amd.provenance import kernel_sources_sha  # noqa: E402
 
 PEAK_GBPS = 8000.0
 
@@ -40,7 +44,7 @@ def main():
         gbps = b / avg[k]
         out[k] = {"hbm_bytes_per_launch": int(b), "avg_launch_ms": round(avg[k] / 1e6, 4),
                   "hbm_gbps": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
-    print(json.dumps({"kernels": out, "peak_gbps": PEAK_GBPS,
+    print(json.dumps({"kernels": out, "peak_gbps": PEAK_GBPS, "sources_sha": kernel_sources_sha(),
                       "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes",
                       "sources": [fetch, write, stats]}, indent=1))
 

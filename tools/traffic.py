@@ -22,6 +22,9 @@ import json
 import sys
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from optixpathtracer_amd.provenance import kernel_sources_sha  # noqa: E402
+
 # dominant kernels: the megakernel, or the wavefront's trace kernels taken as one group
 GROUPS = {"k_render_mega": ("k_render_mega",), "k_extend+k_trace_pair": ("k_extend", "k_trace_pair")}
 
@@ -82,6 +85,8 @@ def main():
         "kernel_trace": stats.get(kernel),
         # the same bench on one wavefront stream (tools/profile.sh kt1): solo launch times
         "kernel_trace_single_stream": kernel_stats(root / "kt1").get(kernel) if (root / "kt1").exists() else None,
+        # the kernel sources these passes ran (bench.py reports the figures only on the same sources)
+        "sources_sha": kernel_sources_sha(),
         "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes; low: FETCH_SIZE + "
                       "WRITE_SIZE (gathers are not half-counted, profiles/r02_hbm_calib.json)",
     }, indent=1))
