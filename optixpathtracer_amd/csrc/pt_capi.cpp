@@ -186,6 +186,8 @@ struct pt_renderer {
         S.n_nodes = bvh_nodes;
         S.lds_nodes = nullptr;
         S.n_lds = 0;
+        S.n_mats = std::max(1, nmesh);
+        S.mat_lds = 0;
         return S;
     }
     float* accum() const { return user_accum ? user_accum : d_accum; }
