@@ -45,8 +45,6 @@ struct WFState {
                                             // queue order of the even bounces (fused modes)
     float4* beta_q = nullptr;               // fused modes: throughput | seed of the odd bounces' queues
     float4* L = nullptr;                    // path radiance of the frame, path order
-    float4* lq[2] = {nullptr, nullptr};     // PT_L_QUEUE fused modes: radiance so far, queue order of
-                                            // the even / odd bounces (ping-pong like beta)
     float4* sh_o = nullptr;                 // shadow queue: origin | path
     float4* sh_d = nullptr;                 // direction | tmax
     float4* sh_c = nullptr;                 // deferred NEE contribution (fused modes)

@@ -115,23 +115,6 @@ __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.c
 // by path: a random 16-B read costs a 64-B line fetch (DESIGN.md §4 counter calibration).
 // Queue 0 is in path order, so k_camera's W.beta[q] serves both layouts.
 __device__ __forceinline__ float4* queue_beta(const WFState& W, int b) { return (b & 1) ? W.beta_q : W.beta; }
-// PT_L_QUEUE (fused modes): a live path's radiance travels in queue order next to its ray
-// (W.lq, ping-pong like queue_beta) instead of sitting in W.L by path, so the deferred NEE add
-// of an unoccluded shadow ray whose path continues is a read-modify-write of its continuation's
-// queue slot -- neighbouring shadow rays touch neighbouring slots -- not a random 16-B RMW of
-// W.L (a line fetch and a 32-B write granule each, DESIGN.md §4 counter calibration).  A path
-// writes W.L[path] once, when it ends.
-#ifndef PT_L_QUEUE
-#define PT_L_QUEUE 0
-#endif
-constexpr bool lq_mode(int mode) {
-    return PT_L_QUEUE && (mode == kModeLambert || mode == kModeConductor || mode == kModeDielectric);
-}
-__device__ __forceinline__ float4* queue_L(const WFState& W, int b) { return W.lq[b & 1]; }
-// sh_c.w of a shadow ray: -1 = the path ends at this bounce (origin in sh_o, add into W.L[path]);
-// otherwise the index of the path's continuation ray in queue b + 1, with kShOrigin = the shadow
-// ray starts at that ray's origin (Lambert) and kShLq = add into queue_L(b + 1)[qi] (PT_L_QUEUE)
-constexpr int kShOrigin = 1 << 30, kShLq = 1 << 29, kShIndex = (1 << 29) - 1;
 inline size_t count_bytes(int max_bounces) { return sizeof(int) * kCntStride * kCnt * (size_t)(max_bounces + 2); }
 
 // Shading kernels: 1024-thread blocks, one queue item per thread over a grid sized to the
@@ -290,15 +273,10 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
                           // with them 12 / 16 / 20 / 32: -1 / 0 / -0 / -5 %)
 #endif
 constexpr int kRefillMin = PT_REFILL_MIN;
-#ifndef PT_SPLIT_FINISH
-#define PT_SPLIT_FINISH 0
+#ifndef PT_SPLIT_FINISH  // k_trace_pair's deferred NEE add as load + store around the refill:
+#define PT_SPLIT_FINISH 1  // +2.2 % Lambert, +1.3 % Conductor, +0.4 % Dielectric
 #endif
-#ifndef PT_PROBE_NO_NEE_ADD  // timing probe only (wrong images): no deferred NEE add in k_trace_pair
-#define PT_PROBE_NO_NEE_ADD 0
-#endif
-#ifndef PT_BATCH_HANDOFF
-#define PT_BATCH_HANDOFF 0
-#endif
+
 #ifndef PT_TRI_BATCH
 #define PT_TRI_BATCH 20  // lanes with a pending leaf before a wave runs its triangle batch (8 / 12 / 16 /
                          // 20 / 24 / 32: -7 / -2 / -0.3 / 0 / -0.3 / -5 %)
@@ -404,15 +382,6 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         if (tri_ok && n_leaf > 0) {  // wave-uniform
             wave_tri_batch<ANY, STATS, TEX>(S, st, active && st.leaf != kEmptyChild, tri_lds, ts);
             if (active && is_any<ANY>(st) && st.h.tri >= 0) done = true;
-#if PT_BATCH_HANDOFF
-            // a lane whose node slot held a leaf while its leaf slot was full (blocked) hands
-            // that leaf over now -- the batch emptied every leaf slot -- and takes the next stack
-            // entry, so it visits a node in this iteration's node half instead of idling in it
-            if (active && !done && st.cur < 0 && st.cur != kEmptyChild) {
-                st.leaf = st.cur;
-                stack_pop<kStack>(st, stk, kBlockWF, spill);
-            }
-#endif
         }
         if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockWF, spill, ts)) done = true;
     }
@@ -549,7 +518,6 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
     // cost them 1-2 %, so they gather it by path
     constexpr bool kBetaQ = MODE == kModeLambert;
     constexpr bool kShareOrigin = MODE == kModeLambert;
-    constexpr bool kLQ = lq_mode(MODE);  // radiance in queue order (PT_L_QUEUE)
     constexpr int kBlock = shf_block(MODE), kWaves = kBlock / 64;
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
@@ -567,14 +535,11 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
         float stmax = 0.0f;
         int path = 0;
         const int P1 = L.width * L.height;
-        // the path's radiance: shade0 -> after bounce 0; kLQ -> so far (queue_L holds it with the
-        // previous bounce's unoccluded NEE added by k_trace_pair), then after this bounce's table NEE
-        float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // shade0: the path's radiance after bounce 0
         if (valid) {
             const float4 hv = ldqs(W.hit + i);
             path = __float_as_int(hv.x);
             const Hit h = decode_hit(hv);
-            if (kLQ && !shade0 && b > 0) l0 = ldqs(queue_L(W, b) + i);  // bounce 0: 0 (k_camera)
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
                 const float4 c = ldqs(rd + (shade0 ? path % P1 : i));
                 d = mk(c.x, c.y, c.z);
@@ -589,7 +554,7 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
                     beta = mk(bv.x, bv.y, bv.z);
                 }
                 if (path == debug_path_id(L)) {  // pt_set_debug_pixel (devicePrograms.cu:637-644)
-                    const float4 l = (shade0 || kLQ) ? l0 : W.L[path];
+                    const float4 l = shade0 ? l0 : W.L[path];
                     debug_record(L, b + 1, __float_as_int(S.isect[3 * h.tri].w), sf, beta, mk(l.x, l.y, l.z));
                 }
                 const bool conductor = rnd(seed) < sf.metallic;  // :400
@@ -611,9 +576,9 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
                         contrib = ((beta * spectrum) * Li) / (P * 1.0f);
                         if (vis0) {  // bounce 0: the (pixel, light) visibility is already known
                             if (W.vis[vis0_index(L, path, li)]) {
-                                const float4 l = (shade0 || kLQ) ? l0 : W.L[path];
+                                const float4 l = shade0 ? l0 : W.L[path];
                                 l0 = make_float4(l.x + contrib.x, l.y + contrib.y, l.z + contrib.z, 0.0f);
-                                if (!shade0 && !kLQ) W.L[path] = l0;
+                                if (!shade0) W.L[path] = l0;
                             }
                         } else {
                             so = sf.pos + 1e-3f * sf.ng;
@@ -632,29 +597,23 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
                 }
             }
         }
-        // shade0: every path of the batch, hit or miss; kLQ: the paths that end at this bounce
-        // (their last shadow ray, if any, adds into W.L[path] in k_trace_pair)
-        if (valid && (kLQ ? !emit_next : shade0)) W.L[path] = l0;
+        if (shade0 && valid) W.L[path] = l0;  // every path of the batch, hit or miss
         const int qi = block_append<kWaves>(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
             if (kBetaQ) stqs(queue_beta(W, b + 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
-            if (kLQ) stqs(queue_L(W, b + 1) + qi, l0);
         }
         const int si = block_append<kWaves>(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
         if (emit_shadow) {
             // Lambert: a sampled direction is never below the surface (lambert_sample forces z >= 0),
             // so the continuation ray starts at the shadow ray's origin (sf.pos + 1e-3 * Ng, the
             // same expression): the shadow record names that ray (qi) instead of repeating origin
-            // and path, and k_trace_pair reads them from the extension queue (kShOrigin).  kLQ: an
-            // unoccluded contribution of a continuing path is added to its continuation's
-            // queue_L slot (kShLq).  -1: the path ends here (own sh_o record, add into W.L).
+            // and path, and k_trace_pair reads them from the extension queue.  -1: own sh_o record.
             const bool share = kShareOrigin && emit_next;
-            const int code = emit_next && (kShareOrigin || kLQ) ? qi | (share ? kShOrigin : 0) | (kLQ ? kShLq : 0) : -1;
             if (!share) stqs(W.sh_o + si, make_float4(so.x, so.y, so.z, __int_as_float(path)));
             stqs(W.sh_d + si, make_float4(sdir.x, sdir.y, sdir.z, stmax));
-            stqs(W.sh_c + si, make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(code)));
+            stqs(W.sh_c + si, make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(share ? qi : -1)));
         }
     }
 }
@@ -667,7 +626,6 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S, DevLaunch L, WFState W, int nf) {
     constexpr bool kBetaQ = MODE == kModeLambert;  // as k_shade_fused
-    constexpr bool kLQ = lq_mode(MODE);
     constexpr int kBlock = shf_block(MODE), kWaves = kBlock / 64;
     const int P1 = L.width * L.height;
     __shared__ int lds_q[kWaves + 1];
@@ -721,13 +679,12 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
                 if (!kBetaQ) stqs(W.beta + path, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
             }
         }
-        if (valid && !(kLQ && emit_next)) stqs(W.L + path, l0);  // every path (kLQ: that ends here)
+        if (valid) stqs(W.L + path, l0);  // every path of the batch, hit or miss
         const int qi = block_append<kWaves>(cnt(W, 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
             if (kBetaQ) stqs(queue_beta(W, 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
-            if (kLQ) stqs(queue_L(W, 1) + qi, l0);
         }
     }
 }
@@ -759,21 +716,19 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
             const int j = i - n_ext;
             const float4 c = W.sh_d[j], k = W.sh_c[j];
             // origin | path: the shadow ray's own record, or (Lambert) the continuation ray of the
-            // same path, which starts at the same point (k_shade_fused, kShOrigin)
+            // same path, which starts at the same point (k_shade_fused)
             const int q = __float_as_int(k.w);
-            const float4 a = (q >= 0 && (q & kShOrigin)) ? ro[q & kShIndex] : W.sh_o[j];
+            const float4 a = q >= 0 ? ro[q] : W.sh_o[j];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
             st.any = true;
-            // an any-hit traversal only writes h.tri: the record's other fields carry where the
-            // contribution goes (the path, or ~the continuation's queue_L slot) and the
-            // contribution to finish()
-            st.h.orig = (q >= 0 && (q & kShLq)) ? ~(q & kShIndex) : __float_as_int(a.w);
+            // an any-hit traversal only writes h.tri: the record's other fields carry the path
+            // and the contribution to finish()
+            st.h.orig = __float_as_int(a.w);
             st.h.t = k.x;
             st.h.u = k.y;
             st.h.v = k.z;
         }
     };
-    float4* const lq_next = queue_L(W, b + 1);  // PT_L_QUEUE: radiance slots of queue b + 1
 #if PT_SPLIT_FINISH
     // the deferred NEE add as load (finish, before the refill's record loads) + store (commit,
     // after them): the lane does not wait for the radiance line before the refill
@@ -789,7 +744,7 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
         if (i < n_ext) W.hit[i] = hit_record(h, st.path);
         __builtin_amdgcn_sched_barrier(0);
         if (i >= n_ext && h.tri < 0) {  // unoccluded: add the deferred NEE contribution
-            a.p = (PT_L_QUEUE && h.orig < 0) ? lq_next + ~h.orig : W.L + h.orig;
+            a.p = W.L + h.orig;
             a.v = *a.p;
             a.x = h.t;
             a.y = h.u;
@@ -805,10 +760,9 @@ __global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene
         const Hit& h = st.h;
         if (i < n_ext) {
             W.hit[i] = hit_record(h, st.path);
-        } else if (h.tri < 0 && !PT_PROBE_NO_NEE_ADD) {  // unoccluded: add the deferred NEE contribution
-            float4* l = (PT_L_QUEUE && h.orig < 0) ? lq_next + ~h.orig : W.L + h.orig;
-            const float4 v = *l;
-            *l = make_float4(v.x + h.t, v.y + h.u, v.z + h.v, 0.0f);
+        } else if (h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+            const float4 l = W.L[h.orig];
+            W.L[h.orig] = make_float4(l.x + h.t, l.y + h.u, l.z + h.v, 0.0f);
         }
     };
     auto commit = NoCommit{};
@@ -1217,8 +1171,7 @@ hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStre
 
 size_t wavefront_bytes(int paths, int max_bounces) {
     size_t P = (size_t)paths;
-    return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 3 /*beta x2, L*/ + 3 /*shadow*/ +
-                                 (PT_L_QUEUE ? 2 : 0) /*radiance x2 queues*/) +
+    return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 3 /*beta x2, L*/ + 3 /*shadow*/) +
            P * (2 + 2 * kShadeBuckets) * sizeof(int) + count_bytes(max_bounces);
 }
 
@@ -1239,10 +1192,6 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
     al((void**)&W.sh_o, P * sizeof(float4));
     al((void**)&W.sh_d, P * sizeof(float4));
     al((void**)&W.sh_c, P * sizeof(float4));
-    if (PT_L_QUEUE) {
-        al((void**)&W.lq[0], P * sizeof(float4));
-        al((void**)&W.lq[1], P * sizeof(float4));
-    }
     al((void**)&W.aux, P * sizeof(int));
     al((void**)&W.vis, P * sizeof(int));
     al((void**)&W.nq, P * kShadeBuckets * sizeof(int));
@@ -1262,7 +1211,7 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
 
 void wavefront_free(WFState& W) {
     void* ps[] = {W.ray_o[0], W.ray_o[1], W.ray_d[0], W.ray_d[1], W.hit, W.beta, W.beta_q, W.L, W.sh_o, W.sh_d, W.sh_c,
-                  W.lq[0], W.lq[1], W.aux, W.vis, W.nq, W.sq, W.count};
+                  W.aux, W.vis, W.nq, W.sq, W.count};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     W = WFState{};
