@@ -13,16 +13,16 @@ cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
 echo "[profile] kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --reference-loops 0 $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
 echo "[profile] kernel trace, one stream (solo kernel times: tools/shade_pmc.py, roofline.single_stream)"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt1" -o run -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --wavefront-streams 1 $ARGS > "$OUT/kt1_bench.json" 2> "$OUT/kt1_bench.log"
+  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --reference-loops 0 --wavefront-streams 1 $ARGS > "$OUT/kt1_bench.json" 2> "$OUT/kt1_bench.log"
 echo "[profile] FETCH_SIZE"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
-  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check $ARGS > "$OUT/fetch.json" 2> "$OUT/fetch.log"
+  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check --reference-loops 0 $ARGS > "$OUT/fetch.json" 2> "$OUT/fetch.log"
 echo "[profile] WRITE_SIZE"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
-  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check $ARGS > "$OUT/write.json" 2> "$OUT/write.log"
+  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check --reference-loops 0 $ARGS > "$OUT/write.json" 2> "$OUT/write.log"
 python3 tools/traffic.py "$OUT" > "$OUT/traffic.json"
 cat "$OUT/traffic.json"
 echo "[profile] done"
