@@ -613,19 +613,15 @@ __device__ __forceinline__ void wave_tri_batch(const DevScene& S, TravState& s, 
         const f3 o = mk(__shfl(s.o.x, owner, 64), __shfl(s.o.y, owner, 64), __shfl(s.o.z, owner, 64));
         const f3 d = mk(__shfl(s.d.x, owner, 64), __shfl(s.d.y, owner, 64), __shfl(s.d.z, owner, 64));
         const float tmax = __shfl(s.best, owner, 64);
-        bool hit = false, bk = false;
-        float t = 0.0f, u = 0.0f, v = 0.0f;
-        int oi = 0;
-        float4 A = make_float4(0.0f, 0.0f, 0.0f, 0.0f), E1 = A, E2 = A;
-        if (valid) {
-            if (STATS) ts.tris++;
-            A = S.isect[3 * ti];
-            E1 = S.isect[3 * ti + 1];
-            E2 = S.isect[3 * ti + 2];
-            hit = tri_test(A, E1, E2, o, d, 0.0f, tmax, t, u, v, bk);
-            if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
-            oi = __float_as_int(A.w);
-        }
+        // every lane tests a triangle: a lane past the end repeats pair 0 (a real pair) and
+        // discards its result, so the round needs no branch and no zeroed registers
+        bool bk = false;
+        float t, u, v;
+        if (STATS && valid) ts.tris++;
+        const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+        bool hit = tri_test(A, E1, E2, o, d, 0.0f, tmax, t, u, v, bk) && valid;
+        if (TEX && hit && __float_as_int(E2.w) != 0) hit = !alpha_cut(S, ti, __float_as_int(E1.w), u, v);
+        const int oi = __float_as_int(A.w);
         // Every candidate is held to the acceptance rule here (tri_accept with the owner's inv / io,
         // read across lanes by the whole wave), so the batch only ever takes acceptable hits: the
         // traversal is strict from the start and its finished rays need no check and no re-trace.
