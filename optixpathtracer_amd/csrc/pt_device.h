@@ -122,11 +122,36 @@ struct Hit {
     bool back;
 };
 
+// PT_CYCLE_PROBE (timing probe of the wavefront trace loop, with traversal stats on): the
+// wave_active_lanes / wave_node_steps / wave_tri_steps / wave_refills counters hold the shader
+// cycles each wave spent waiting for the node half's loads, in the rest of the node half, in the
+// triangle batches and in the refill blocks (s_memtime around each section; a section's end
+// waits for a value it produced, so its memory operations have landed).
+#ifndef PT_CYCLE_PROBE
+#define PT_CYCLE_PROBE 0
+#endif
+__device__ __forceinline__ uint64_t probe_clock() {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+template <class T>
+__device__ __forceinline__ uint64_t probe_clock(const T& dep) {  // once `dep` is available
+    T v = dep;
+    __asm__ volatile("" : "+v"(v));
+    __builtin_amdgcn_s_waitcnt(0);
+    return probe_clock();
+}
+
 struct TravStats {
     uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0, retrace = 0;
     // wave schedule (trace_range, lane 0 of each wave): iterations, active lanes summed over
     // them, iterations running the node half / the triangle half, refill blocks
     uint32_t steps = 0, active = 0, node_steps = 0, tri_steps = 0, refills = 0;
+#if PT_CYCLE_PROBE
+    uint64_t probe_t = 0;  // s_memtime when the node half's loads landed
+#endif
 };
 
 // ---- ray / box arithmetic shared bit for bit with the oracle ---------------------------------
@@ -196,7 +221,7 @@ constexpr int kSpillDepth = 64;
 // LDS stack depths of the wavefront trace kernels and of the megakernel / k_trace (A/B builds
 // override them with -D; every translation unit sees the same value)
 #ifndef PT_WF_STACK
-#define PT_WF_STACK 14
+#define PT_WF_STACK 11  // 6 trace workgroups per CU (14 at 5 per CU before)
 #endif
 #ifndef PT_MK_STACK
 #define PT_MK_STACK 32
@@ -576,7 +601,8 @@ constexpr int kTriPairsPerWave = 256;  // 64 lanes x <= 4 triangles per leaf
 struct TriBatchLds {                    // one per wave
     uint32_t pair[kTriPairsPerWave];    // (leaf-order triangle << 6) | owner lane
     unsigned long long key[64];         // per owner: min over this round's hits of (t bits << 32 | orig)
-    float4 res[64];                     // per owner: the winning pair's u, v, tri | back << 31
+    float2 res_uv[64];                  // per owner: the winning pair's u, v
+    int res_code[64];                   //   and tri | back << 31 (2.25 KB per wave in all)
 };
 
 __device__ __forceinline__ int lane_prefix(unsigned long long m) {
@@ -638,13 +664,17 @@ __device__ __forceinline__ void wave_tri_batch(const DevScene& S, TravState& s, 
         if (hit) atomicMin(&L->key[owner], key);
         __builtin_amdgcn_wave_barrier();
         if (hit && L->key[owner] == key)  // the owner's winning pair (a triangle is in one leaf only)
-            L->res[owner] = make_float4(u, v, __int_as_float(ti | (bk ? (int)0x80000000 : 0)), 0.0f);
+        {
+            L->res_uv[owner] = make_float2(u, v);
+            L->res_code[owner] = ti | (bk ? (int)0x80000000 : 0);
+        }
         __builtin_amdgcn_wave_barrier();
         const unsigned long long w = L->key[lane];
         if (w != ~0ull) {
             const float tw = __uint_as_float((uint32_t)(w >> 32));
             const int ow = (int)(uint32_t)w;
-            const float4 r = L->res[lane];
+            const float2 ruv = L->res_uv[lane];
+            const float4 r = make_float4(ruv.x, ruv.y, __int_as_float(L->res_code[lane]), 0.0f);
             const int code = __float_as_int(r.z);
             if (flags & 2) {  // (this lane's own kind) any hit: done; only h.tri (the record's other fields carry the path)
                 s.h.tri = code & 0x7fffffff;
@@ -672,7 +702,11 @@ __device__ __forceinline__ bool trav_node_step(const DevScene& S, TravState& s, 
         if (STATS) ts.nodes++;
         float t0, t1, t2, t3;
         int c0, c1, c2, c3;
-        node_eval(node_load(S, s, s.cur), s, t0, t1, t2, t3, c0, c1, c2, c3);
+        const NodeLoad nl = node_load(S, s, s.cur);
+#if PT_CYCLE_PROBE
+        if (STATS) ts.probe_t = probe_clock(nl.ch.x);
+#endif
+        node_eval(nl, s, t0, t1, t2, t3, c0, c1, c2, c3);
         if (ANY != kRayAny) {
             cswap(t0, c0, t1, c1);
             cswap(t2, c2, t3, c3);

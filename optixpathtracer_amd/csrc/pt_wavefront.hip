@@ -39,25 +39,25 @@ namespace pt {
 namespace {
 
 constexpr int kBlockWF = 256;
-// LDS traversal stack entries per lane (PT_WF_STACK, pt_device.h): 14 KB per workgroup keeps
-// the trace kernels VGPR-limited rather than LDS-limited (deeper entries spill).
+// LDS traversal stack entries per lane (PT_WF_STACK, pt_device.h): 11 KB per workgroup.
 constexpr int kStack = PT_WF_STACK;
-// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 57 =
-// the three top levels (21) and 36 of the fourth, 7.1 KB).  With the 14-KB stack and the 10-KB
-// triangle batches (below) a workgroup takes 31.7 KB, so a CU still holds the 5 workgroups its
-// VGPRs allow.  Sweeps on the v34 tree: 0 / 21 / 41 / 85 nodes with a 16-entry
-// stack -8.6 / -1.2 / 0 / -7.5 % Lambert (85: LDS-limited); 57 nodes with 14 stack entries
-// +1.2 %, 73 with 12 +0.5 %.
+// Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 49 =
+// the three top levels (21) and 28 of the fourth, 6.1 KB).  With the 11-KB stack and the 9-KB
+// triangle batches (below) a workgroup takes 26.1 KB, so a CU holds 6 workgroups, the 6 waves per
+// SIMD the kernels' 80 VGPRs allow (v39, DESIGN.md §5: Lambert +2.4 %, Conductor +7.7 %,
+// Dielectric +4.5 % over 5 waves with 14 entries and 57 nodes; the kernels wait on memory in
+// more than half their cycles, and a sixth wave covers more of it).  Earlier sweeps at 5 waves
+// (v34 tree): 0 / 21 / 41 / 85 nodes with a 16-entry stack -8.6 / -1.2 / 0 / -7.5 % Lambert.
 #ifndef PT_LDS_NODES
-#define PT_LDS_NODES 57
+#define PT_LDS_NODES 49
 #endif
 constexpr int kLdsNodes = PT_LDS_NODES;
-// wave-batched triangle tests (pt_device.h wave_tri_batch): 2.5 KB of LDS per wave
+// wave-batched triangle tests (pt_device.h wave_tri_batch): 2.25 KB of LDS per wave
 constexpr int kTriBatchWaves = kBlockWF / 64;
-// Trace kernels: 5 waves per SIMD (96 VGPRs, no spills); the textured variants spill a few
-// VGPRs at 96 and keep 4.
+// Trace kernels: 6 waves per SIMD (80 VGPRs, 3 spilled in cold paths); the textured variants
+// keep 4.
 #ifndef PT_WF_WAVES
-#define PT_WF_WAVES 5
+#define PT_WF_WAVES 6
 #endif
 constexpr int wf_waves(bool tex) { return tex ? 4 : PT_WF_WAVES; }
 constexpr int kMissTri = -1;
@@ -335,7 +335,11 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         // batch block once enough lanes idle (it costs the wave about as much as a step), and
         // at every step once the slice is drained
         if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
+#if PT_CYCLE_PROBE
+            const uint64_t c0 = probe_clock();
+#else
             if (STATS) ts.refills++;
+#endif
             TokS tok{};
             const bool fin = done;
             if (done) {  // the triangle batches took acceptable hits only: the answer stands
@@ -358,6 +362,9 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
             if constexpr (kSplit) {
                 if (fin) commit(tok);
             }
+#if PT_CYCLE_PROBE
+            if (STATS) ts.refills += (uint32_t)(probe_clock(st.best) - c0);
+#endif
         }
         const bool active = ri >= 0 && !done;
         const unsigned long long act = __ballot(active);
@@ -373,17 +380,35 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         const bool tri_ok = n_leaf >= min(PT_TRI_BATCH, n_act) || 2 * n_node < n_act;
         if (STATS) {
             ts.steps++;
+#if !PT_CYCLE_PROBE
             ts.active += n_act;
             ts.node_steps += n_node > 0;
             ts.tri_steps += tri_ok && n_leaf > 0;
+#endif
         }
+#if PT_CYCLE_PROBE
+        const uint64_t c1 = probe_clock();
+#endif
         // the triangles of every pending leaf in one wave batch (pt_device.h wave_tri_batch),
         // then the node half of the step
         if (tri_ok && n_leaf > 0) {  // wave-uniform
             wave_tri_batch<ANY, STATS, TEX>(S, st, active && st.leaf != kEmptyChild, tri_lds, ts);
             if (active && is_any<ANY>(st) && st.h.tri >= 0) done = true;
         }
+#if PT_CYCLE_PROBE
+        const uint64_t c2 = probe_clock(st.best);
+        if (STATS) ts.tri_steps += (uint32_t)(c2 - c1);
+#endif
         if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockWF, spill, ts)) done = true;
+#if PT_CYCLE_PROBE
+        if (STATS) {  // node half: until its loads landed (active), the rest (node_steps)
+            const uint64_t c4 = probe_clock(st.cur);
+            const unsigned long long ml = __ballot(ts.probe_t > c2);
+            const uint64_t tl = ml ? (uint64_t)__shfl((long long)ts.probe_t, __ffsll((long long)ml) - 1, 64) : c2;
+            ts.active += (uint32_t)(tl - c2);
+            ts.node_steps += (uint32_t)(c4 - tl);
+        }
+#endif
     }
 }
 

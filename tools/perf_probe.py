@@ -86,7 +86,10 @@ def main():
                                     "tri_util": round(s["tri_tests"] / (64 * max(1, s["wave_tri_steps"])), 3),
                                     "node_step_frac": round(s["wave_node_steps"] / ws, 3),
                                     "tri_step_frac": round(s["wave_tri_steps"] / ws, 3),
-                                    "refill_frac": round(s["wave_refills"] / ws, 3)})
+                                    "refill_frac": round(s["wave_refills"] / ws, 3),
+                                    # raw counters (a PT_CYCLE_PROBE build puts shader cycles per section here)
+                                    "raw": {k: s[k] for k in ("wave_steps", "wave_active_lanes", "wave_node_steps",
+                                                              "wave_tri_steps", "wave_refills", "rays")}})
                     print(json.dumps(out), flush=True)
         r.close()
 
