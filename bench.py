@@ -322,7 +322,7 @@ def main():
         valu = None  # the VALU fraction beside the HBM roofline, from PMC passes
         vd, cur = pmc_record(ROOT / "profiles" / "valu.json", sha)
         if vd and dom == "k_extend+k_trace_pair" and args.config == "2":
-            fig = {k: vd.get(k) for k in ("kernel", "valu_busy", "lane_utilisation")}
+            fig = {k: vd.get(k) for k in ("kernel", "valu_busy", "valu_issue_slots", "lane_utilisation", "wait_per_wave_cycle")}
             if cur:
                 valu = {**fig, "sources_sha": sha}
             else:
