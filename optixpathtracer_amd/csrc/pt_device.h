@@ -10,7 +10,7 @@
 //   isect  : float4[3N]         — v0.xyz|orig index, e1.xyz|material, e2.xyz|0  (e = v - v0,
 //                                  the same fp32 subtraction the oracle performs)
 //   shade  : float4[4N]         — v1.xyz|n0.x, v2.xyz|n0.y, n0.z n1.xyz, n2.xyz|0
-//   mats   : float4[2M]         — albedo.xyz|metallic, roughness|has_normals|0|0
+//   mats   : float4[3M]         — albedo.xyz|metallic, roughness|has_normals|texture ids, ... (kMatStride)
 // Leaves reference up to 4 consecutive triangles (a BVH subtree is a contiguous range of the
 // leaf-ordered triangles, so no index indirection is needed).
 #pragma once

@@ -563,10 +563,15 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
         float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // shade0: the path's radiance after bounce 0
         if (valid) {
             const float4 hv = ldqs(W.hit + i);
+            // the queue-order records go out beside the hit record instead of after it: they do not
+            // depend on it, and waiting for the hit first put two HBM round trips in a row (Lambert
+            // +2 %)
+            const float4 c_q = shade0 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ldqs(rd + i);
+            const float4 bv_q = (!shade0 && kBetaQ) ? ldqs(queue_beta(W, b) + i) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             path = __float_as_int(hv.x);
             const Hit h = decode_hit(hv);
             if (h.tri >= 0) {  // a miss ends the path (__miss__radiance :576-583)
-                const float4 c = ldqs(rd + (shade0 ? path % P1 : i));
+                const float4 c = shade0 ? ldqs(rd + path % P1) : c_q;
                 d = mk(c.x, c.y, c.z);
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
@@ -574,7 +579,7 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
                     seed = tea16((uint32_t)(path % P1), L.frame_base + (uint32_t)(path / P1));
                     beta = mk(1.0f, 1.0f, 1.0f);
                 } else {
-                    float4 bv = ldqs(kBetaQ ? queue_beta(W, b) + i : W.beta + path);
+                    float4 bv = kBetaQ ? bv_q : ldqs(W.beta + path);
                     seed = __float_as_uint(bv.w);
                     beta = mk(bv.x, bv.y, bv.z);
                 }
@@ -827,10 +832,10 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
     float stmax = 0.0f;
     if (i < n) {
         const float4 hv = W.hit[i];
+        const float4 c = rd[i];  // beside the hit record (as k_shade_fused)
         const int path = __float_as_int(hv.x);
         const Hit h = decode_hit(hv);
         if (h.tri >= 0) {
-            const float4 c = rd[i];
             SurfaceHit sf;
             reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
             float4 bv = W.beta[path];
