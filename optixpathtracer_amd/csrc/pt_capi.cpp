@@ -91,8 +91,8 @@ struct EventPool {
 constexpr int kCounters = 16;
 // event pairs held by one renderer before launch_frames retires them (EventPool)
 constexpr size_t kMaxPendingEvents = 4096;
-// the smallest traversal stack of any kernel (pt_device.h stack_capacity: 77 entries for the
-// wavefront's 14 LDS entries and 64 spill slots in chunks of 7)
+// the smallest traversal stack of any kernel (pt_device.h stack_capacity: 71 entries for the
+// wavefront's 11 LDS entries and 64 spill slots in chunks of 5)
 constexpr int kMinTraversalStack = std::min(stack_capacity(PT_WF_STACK), stack_capacity(PT_MK_STACK));
 
 }  // namespace
