@@ -1,8 +1,5 @@
 set -e
-O=gpurun_out/r03x
-mkdir -p $O
+mkdir -p gpurun_out/r03ze
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-PTAMD_LIB=optixpathtracer_amd/_variants/lib_both.so timeout -k 10 400 python -u -m pytest tests/test_gpu_bitexact.py tests/test_gpu_timed_config.py tests/test_gpu_determinism.py -x -q --timeout 200 --timeout-method thread > $O/test_both.log 2>&1 || { tail -30 $O/test_both.log; exit 1; }
-tail -1 $O/test_both.log
-tools/ab.sh "base hoist spop both" 3 --fpl 64 --spp 256 --modes 1,3,2,0 --repeat 1 > $O/ab.log 2>&1
-python3 tools/ab_summary.py $O/ab.log
+timeout -k 10 300 python3 bench.py > gpurun_out/r03ze/bench_default.json 2> gpurun_out/r03ze/bench_default.log
+cat gpurun_out/r03ze/bench_default.json
