@@ -327,6 +327,14 @@ def main():
                 valu = {**fig, "sources_sha": sha}
             else:
                 pmc_stale["valu_pmc"] = {**fig, "sources_sha": vd.get("sources_sha"), "stale": True}
+        vmem = None  # the vector memory path (TA / TD busy), what the trace kernel waits on
+        md, cur = pmc_record(ROOT / "profiles" / "vmem.json", sha)
+        if md and dom == "k_extend+k_trace_pair" and args.config == "2":
+            fig = {k: md.get(k) for k in ("kernel", "ta_busy", "td_busy", "td_tc_stall", "l2_read_latency_cycles")}
+            if cur:
+                vmem = {**fig, "sources_sha": sha}
+            else:
+                pmc_stale["vmem_pmc"] = {**fig, "sources_sha": md.get("sources_sha"), "stale": True}
         shade = None  # the memory-bound kernel of a Lambert frame, PMC HBM GB/s (tools/shade_pmc.py)
         sd, cur = pmc_record(ROOT / "profiles" / "shade_pmc.json", sha)
         if sd and dom == "k_extend+k_trace_pair" and args.config == "2":
@@ -391,8 +399,10 @@ def main():
                 "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
                 # SURVEY.md §8(d) whole-path figure: (segments*396 + samples*12) / render time
                 "pipeline_gbps": round(alg_bytes / max(kernel_s, 1e-9) / 1e9, 2),
-                # the bound that actually limits the trace kernel (issue-bound)
+                # what limits the trace kernel: latency on the vector memory path,
+                # whose address / data units are near saturation (vmem_pmc), not VALU issue (valu_pmc)
                 "valu_pmc": valu,
+                "vmem_pmc": vmem,
                 # PMC HBM bandwidth of the shading kernel (2 x FETCH_SIZE + WRITE_SIZE per launch)
                 "shade_pmc": shade,
                 "single_stream": single,

@@ -80,6 +80,7 @@ __global__ void k_morton(const float4* tri, int n, float3 cmin, float3 cinv, uin
 
 // Leaf-order gather.  isect: v0|orig, (v1-v0)|material, (v2-v0)|alpha flag — the edge subtraction
 // is the same single fp32 op the oracle performs, so the hit arithmetic stays identical.
+// shade: v1|n0.x, v2|n0.y, n0.z n1, n2|material.
 __global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const float4* uv_orig, const uint32_t* order,
                          int n, float4* isect, float4* shade, float4* tuv, float4* st0, float4* pleaf) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -97,7 +98,7 @@ __global__ void k_gather(const float4* tri_orig, const float4* nrm_orig, const f
     shade[4 * k] = make_float4(b.x, b.y, b.z, na.x);
     shade[4 * k + 1] = make_float4(c.x, c.y, c.z, na.y);
     shade[4 * k + 2] = make_float4(na.z, nb.x, nb.y, nb.z);
-    shade[4 * k + 3] = make_float4(nc.x, nc.y, nc.z, 0.0f);
+    shade[4 * k + 3] = make_float4(nc.x, nc.y, nc.z, b.w);  // w: material (as isect's e1.w) for reconstruct
     float lo[3], hi[3];
     tri_box(tri_orig, i, lo, hi);
     st0[2 * k] = make_float4(lo[0], lo[1], lo[2], 0.0f);

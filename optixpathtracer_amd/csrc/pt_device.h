@@ -853,12 +853,24 @@ __device__ __forceinline__ void apply_textures(const DevScene& S, int ti, float 
 
 // TEX: the scene has textures (kernels are instantiated both ways so untextured scenes keep
 // the texture code out of their register budget).
+#ifndef PT_SHADE_EDGES
+#define PT_SHADE_EDGES 1
+#endif
 template <bool TEX>
 __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 d, SurfaceHit& s) {
     const int ti = h.tri;
-    const float4 A = S.isect[3 * ti], E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
+    const float4 A = S.isect[3 * ti];
     const float4 S0 = S.shade[4 * ti], S1 = S.shade[4 * ti + 1], S2 = S.shade[4 * ti + 2], S3 = S.shade[4 * ti + 3];
+#if PT_SHADE_EDGES
+    // the edges again from the vertices: e = v - v0 is the one fp32 subtraction k_gather stored in
+    // isect, so Ng is bit-identical, and the hit costs five gathers instead of seven
+    const float4 E1 = make_float4(S0.x - A.x, S0.y - A.y, S0.z - A.z, 0.0f);
+    const float4 E2 = make_float4(S1.x - A.x, S1.y - A.y, S1.z - A.z, 0.0f);
+    const int mi = __float_as_int(S3.w);
+#else
+    const float4 E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
     const int mi = __float_as_int(E1.w);
+#endif
     const float4 M0 = mat_load(S, kMatStride * mi), M1 = mat_load(S, kMatStride * mi + 1);
     f3 wo_w = normalize(-d);
     f3 v0 = mk(A.x, A.y, A.z), v1 = mk(S0.x, S0.y, S0.z), v2 = mk(S1.x, S1.y, S1.z);

@@ -54,9 +54,11 @@ def test_pmc_record_only_current_sources(tmp_path):
 
 
 def test_committed_pmc_files_are_tagged():
-    for name in ("traffic.json", "valu.json", "shade_pmc.json"):
+    for name in ("traffic.json", "valu.json", "shade_pmc.json", "vmem.json"):
         d = json.loads((ROOT / "profiles" / name).read_text())
         assert re.fullmatch(r"[0-9a-f]{16}", d.get("sources_sha") or ""), name
     v = json.loads((ROOT / "profiles" / "valu.json").read_text())
     # valu_busy counts two wave64 VALU issues per SIMD quad-cycle (pmc_summary.py)
     assert abs(v["valu_busy"] - v["valu_issue_slots"] / 2) < 1e-3
+    m = json.loads((ROOT / "profiles" / "vmem.json").read_text())
+    assert 0.0 < m["ta_busy"] <= 1.0 and 0.0 < m["td_busy"] <= 1.0

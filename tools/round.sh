@@ -3,7 +3,8 @@
 #   tools/round.sh TAG bench    GPU tests, then bench.py on every BASELINE config
 #   tools/round.sh TAG profile  tools/profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE
 #                               passes) on the headline, then the SQ/TCC/TCP passes of tools/pmc.sh
-#                               for profiles/valu.json
+#                               for profiles/valu.json and the TA/TD passes of tools/pmc_ta.sh for
+#                               profiles/vmem.json
 # Every step has its own time limit and the chain stops at the first failure.
 set -e
 TAG=${1:-r03}
@@ -26,4 +27,7 @@ else
   echo "[round] pmc (SQ / TCC / TCP passes, Lambert, 64 frames)"
   timeout -k 10 600 tools/pmc.sh gpurun_out/pmc_$TAG --fpl 64 --spp 64 > "$OUT/pmc.log" 2>&1
   tail -1 "$OUT/pmc.log"
+  echo "[round] pmc (TA / TD / TCP passes, Lambert, 64 frames)"
+  timeout -k 10 600 tools/pmc_ta.sh gpurun_out/pmcta_$TAG --fpl 64 --spp 64 > "$OUT/pmc_ta.log" 2>&1
+  tail -1 "$OUT/pmc_ta.log"
 fi
