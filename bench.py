@@ -102,7 +102,7 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="override the config's scaling (all configs: strong = the step's spp in total, split "
                          "over the ranks; weak = the step's spp per rank)")
-    ap.add_argument("--reference-loops", type=int, default=64,
+    ap.add_argument("--reference-loops", type=int, default=256,
                     help="pt_render calls (1 spp each, frame.id++, 24.9 MB download per call: the reference's "
                          "OptixView::DrawOptix -> OptixRenderer::Render loop) timed for value_reference_loop; 0 = off")
     a = ap.parse_args()
@@ -418,18 +418,31 @@ def main():
             # OptixView.cpp:201-210, OptixRenderer.cpp:617-647): one pt_render per spp (frame.id++,
             # one 1-frame wavefront batch) and a download of the 24.9 MB frame into a freshly
             # allocated host array every call; the GL upload and blend are not part of it.
+            # pt_render renders ahead (pt_set_render_ahead, default 64 frames: while the render state
+            # is unchanged, a call that misses renders the next 1, 2, 4, ... 64 frame ids in one batch
+            # and later calls download theirs), so the loop is timed from a state change on, ramp
+            # included; the same loop with render-ahead off is reported beside it.
+            def ref_loop(calls):
+                r.frame_id = 0
+                r.Render()  # the first call after a change renders its own frame only
+                t = time.perf_counter()
+                for _ in range(calls):
+                    r.Render(np.empty((args.height, args.width, 3), np.float32))
+                return time.perf_counter() - t
+
             fid = r.frame_id
-            r.frame_id = 0
-            r.Render()  # first call sizes the 1-frame queues
-            t4 = time.perf_counter()
-            for _ in range(args.reference_loops):
-                r.Render(np.empty((args.height, args.width, 3), np.float32))
-            e4 = time.perf_counter() - t4
+            e4 = ref_loop(args.reference_loops)
+            r.set_render_ahead(1)
+            n_off = min(args.reference_loops, 64)
+            e5 = ref_loop(n_off)
+            r.set_render_ahead(64)
             r.frame_id = fid
             out["value_reference_loop"] = round(args.width * args.height * args.reference_loops / e4 / 1e6, 3)
             out["reference_loop"] = {"calls": args.reference_loops, "ms_per_call": round(e4 / args.reference_loops * 1e3, 3),
                                      "what": "pt_render: 1 spp per call, frame.id++, D2H download of the 24.9 MB "
-                                             "frame per call (the reference's DrawOptix loop)"}
+                                             "frame per call (the reference's DrawOptix loop), render-ahead on",
+                                     "no_render_ahead": {"calls": n_off, "ms_per_call": round(e5 / n_off * 1e3, 3),
+                                                         "value": round(args.width * args.height * n_off / e5 / 1e6, 3)}}
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline (oracle) ...")
             band, spp_cpu, out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_baseline_seconds)

@@ -209,6 +209,14 @@ int pt_launch(pt_renderer* r, const pt_launch_params* params);
  * one sample per pixel, synchronous, downloads W*H*3 floats to host_rgb.  No-op before
  * the first pt_resize (as :621). */
 int pt_render(pt_renderer* r, float* host_rgb);
+/* Render-ahead for pt_render / pt_display_add_frame (wavefront kernel; default 64 frames, 1 = off).
+ * While the size, camera, lights, max bounces, material mode, kernel and debug pixel stay the
+ * same between calls, a call whose frame id is not ready renders the next k frame ids as one
+ * batch into a ring of k 1-spp images, k doubling on each such call that continues the sequence
+ * (1, 2, 4, ... up to `frames`) and restarting at 1 after any change; later calls download their
+ * frame from the ring.  Every image is bit-identical to rendering its frame alone; the ring holds
+ * `frames` W*H*3 floats.  Out of device memory it falls back to one frame per call. */
+int pt_set_render_ahead(pt_renderer* r, int32_t frames);
 
 /* Device-resident accumulation (replaces the per-spp download + GL blend of
  * Renderer/OptixView.cpp:201-255 / AddPathtracedFrame.frag:18-24).  Renders frame ids

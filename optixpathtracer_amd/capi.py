@@ -162,6 +162,7 @@ SIGNATURES = {
     "pt_set_material_mode": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel": (C.c_int, [_R, C.c_int32]),
     "pt_set_frames_per_launch": (C.c_int, [_R, C.c_int32]),
+    "pt_set_render_ahead": (C.c_int, [_R, C.c_int32]),
     "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel_timing": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),

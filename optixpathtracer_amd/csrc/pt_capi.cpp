@@ -135,6 +135,27 @@ struct pt_renderer {
     uint32_t* d_texels = nullptr;  // RGBA8 texel pool
     int4* d_texinfo = nullptr;     // per texture: offset, width, height
     float* d_frame = nullptr;   // 1-spp frame (pt_render)
+    // render-ahead (pt_set_render_ahead): while nothing that changes the image changes between
+    // pt_render calls, a miss renders the next k frames in one wavefront batch into a ring of
+    // 1-spp images (k doubling per sequential miss up to render_ahead), and the calls for those
+    // frame ids download them from the ring
+    struct RenderKey {
+        int w = 0, h = 0, n_lights = 0, max_bounces = 0, mode = 0, kernel = 0, debug_pixel = -1;
+        uint32_t lights_version = 0, debug_frame = 0;
+        const void* lights = nullptr;
+        float cam[3 + 16 + 16] = {};
+        bool operator==(const RenderKey& o) const {
+            return w == o.w && h == o.h && n_lights == o.n_lights && max_bounces == o.max_bounces && mode == o.mode &&
+                   kernel == o.kernel && debug_pixel == o.debug_pixel && lights_version == o.lights_version &&
+                   debug_frame == o.debug_frame && lights == o.lights && std::memcmp(cam, o.cam, sizeof cam) == 0;
+        }
+    };
+    int render_ahead = 64;
+    float* d_ring = nullptr;
+    int ring_cap = 0, ring_k = 1;
+    uint32_t ring_first = 0, ring_n = 0;
+    RenderKey ring_key;
+    uint32_t lights_version = 0;
     float* d_display = nullptr;  // progressive view buffer (pt_display_*)
     int display_max = -1;
     int display_samples = 0;
@@ -216,7 +237,7 @@ int next_event_pair(pt_renderer* r, hipEvent_t* a, hipEvent_t* b) {
 }
 
 DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, uint32_t n_frames,
-                      double* accum64 = nullptr) {
+                      double* accum64 = nullptr, size_t frame_stride = 0) {
     DevLaunch L;
     L.width = r->width;
     L.height = r->height;
@@ -230,6 +251,7 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
     L.n_frames = n_frames;
     L.accum = accum;
     L.accum64 = accum64;
+    L.frame_stride = frame_stride;
     L.counters = r->d_counters;
     L.debug_pixel = r->d_debug ? r->debug_pixel : -1;
     L.debug_frame = r->debug_frame;
@@ -240,7 +262,9 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
 // Launch frames [first, first+n) in chunks, adding into accum; brackets with events.  Does not
 // wait for earlier work: the event pairs of every launch since the last synchronisation point
 // are summed at the next pt_synchronize / pt_get_stats / download (collect_pending).
-int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, double* accum64 = nullptr) {
+// frame_stride > 0 (wavefront only): frame first + j is written alone to accum + j * frame_stride.
+int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, double* accum64 = nullptr,
+                  size_t frame_stride = 0) {
     int rc = PT_OK;
     // callers that never synchronise through the library (pt_stream interop, device sum buffers,
     // loops over pt_launch / pt_display_add_frame) would grow the event pools without bound:
@@ -257,6 +281,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
     if (kernel == PT_KERNEL_AUTO) kernel = PT_KERNEL_WAVEFRONT;
     if (accum64 && kernel != PT_KERNEL_WAVEFRONT)
         return fail(PT_ERR_INVALID, "fp64 accumulation (pt_set_accum_fp64) runs with the wavefront kernel");
+    if (frame_stride && kernel != PT_KERNEL_WAVEFRONT)
+        return fail(PT_ERR_INVALID, "per-frame images (render-ahead) run with the wavefront kernel");
     if (kernel == PT_KERNEL_WAVEFRONT) {
         // Frames per wavefront launch chain: the queues hold nf frames' paths (208 B each), at most
         // kMaxWFPaths of them.  Batching amortises launch gaps and the per-kernel SIMT tail:
@@ -310,7 +336,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         int batch = 0;
         for (uint32_t f = 0; f < n; ++batch) {  // one event pair per batch (the batch's kernel chain)
             const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
-            DevLaunch L = make_launch(r, accum, first + f, (uint32_t)nf, accum64);
+            DevLaunch L = make_launch(r, frame_stride ? accum + (size_t)f * frame_stride : accum, first + f,
+                                      (uint32_t)nf, accum64, frame_stride);
             const int sk = batch % ns;  // stream of this batch
             hipStream_t st = r->wf_stream(sk);
             if (!dual) {
@@ -361,6 +388,90 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
 }
 
 bool valid_mode(int m) { return m >= PT_MAT_DEFAULT && m <= PT_MAT_LAYERED; }
+
+// Everything a 1-spp image depends on besides its frame id (the scene is fixed at pt_create).
+pt_renderer::RenderKey render_key(const pt_renderer* r) {
+    pt_renderer::RenderKey k;
+    k.w = r->width;
+    k.h = r->height;
+    k.n_lights = r->n_lights;
+    k.max_bounces = r->max_bounces;
+    k.mode = r->material_mode;
+    k.kernel = r->kernel;
+    k.debug_pixel = r->d_debug ? r->debug_pixel : -1;
+    k.debug_frame = r->debug_frame;
+    k.lights_version = r->lights_version;
+    k.lights = r->d_lights;
+    std::memcpy(k.cam, r->cam_pos, sizeof r->cam_pos);
+    std::memcpy(k.cam + 3, r->inv_view, sizeof r->inv_view);
+    std::memcpy(k.cam + 19, r->inv_proj, sizeof r->inv_proj);
+    return k;
+}
+
+void ring_free(pt_renderer* r) {
+    if (r->d_ring) (void)hipFree(r->d_ring);
+    r->d_ring = nullptr;
+    r->ring_cap = 0;
+    r->ring_n = 0;
+    r->ring_k = 1;
+}
+
+// The 1-spp image of frame r->frame_id for pt_render / pt_display_add_frame (OptixRenderer::Render,
+// OptixRenderer.cpp:617-647), enqueued on r->stream.  With render-ahead (wavefront kernel), a frame
+// the ring holds under the same render state is taken from it; a miss renders the next k frames
+// as one batch into the ring, k doubling on every miss that continues the ring's frame sequence
+// under the same state (up to r->render_ahead) and 1 otherwise, so an interactive caller that
+// changes the camera every frame pays for one frame per call.  Each ring image is the one-frame
+// sum into zeros that the plain path computes, bit for bit.
+int render_frame_image(pt_renderer* r, const float** img) {
+    const size_t n3 = 3 * (size_t)r->width * (size_t)r->height;
+    const int kernel = r->kernel == PT_KERNEL_AUTO ? PT_KERNEL_WAVEFRONT : r->kernel;
+    const uint32_t f = r->frame_id;
+    if (r->render_ahead > 1 && kernel == PT_KERNEL_WAVEFRONT) {
+        const pt_renderer::RenderKey k = render_key(r);
+        const bool same = r->ring_n > 0 && k == r->ring_key;
+        if (same && f - r->ring_first < r->ring_n) {  // unsigned: also false for f < ring_first
+            *img = r->d_ring + (size_t)(f - r->ring_first) * n3;
+            return PT_OK;
+        }
+        const bool seq = same && f == r->ring_first + r->ring_n;
+        const int kf = seq ? std::min(2 * r->ring_k, r->render_ahead) : 1;
+        r->ring_n = 0;
+        int rc = PT_OK;
+        if (kf > r->ring_cap) {  // one frame first, then the whole ring
+            const int cap = kf == 1 ? 1 : r->render_ahead;
+            if (r->d_ring) {
+                PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+                (void)hipFree(r->d_ring);
+                r->d_ring = nullptr;
+                r->ring_cap = 0;
+            }
+            const hipError_t e = hipMalloc(&r->d_ring, sizeof(float) * n3 * (size_t)cap);
+            if (e == hipSuccess)
+                r->ring_cap = cap;
+            else
+                rc = hip_fail(e, "hipMalloc render-ahead ring");
+        }
+        if (rc == PT_OK) rc = launch_frames(r, r->d_ring, f, (uint32_t)kf, nullptr, n3);
+        if (rc == PT_OK) {
+            r->ring_key = k;
+            r->ring_first = f;
+            r->ring_n = (uint32_t)kf;
+            r->ring_k = kf;
+            *img = r->d_ring;
+            return PT_OK;
+        }
+        if (rc != PT_ERR_NOMEM) return rc;
+        // no room for the ring or its k-frame queues: render frame by frame from here on
+        ring_free(r);
+        r->render_ahead = 1;
+    }
+    PT_HIP(hipMemsetAsync(r->d_frame, 0, sizeof(float) * n3, r->stream), "hipMemset frame");
+    const int rc = launch_frames(r, r->d_frame, f, 1);
+    if (rc) return rc;
+    *img = r->d_frame;
+    return PT_OK;
+}
 
 // Multi-device pt_render_frames: frame ids first .. first+n-1 split into contiguous blocks
 // (device g renders first + g*n/N .. , the same split as optixpathtracer_amd/sharding.py), each
@@ -688,6 +799,7 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_texinfo) (void)hipFree(r->d_texinfo);
     if (r->d_lights) (void)hipFree(r->d_lights);
     if (r->d_frame) (void)hipFree(r->d_frame);
+    ring_free(r);
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_display) (void)hipFree(r->d_display);
     if (r->d_counters) (void)hipFree(r->d_counters);
@@ -719,6 +831,7 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     size_t bytes = sizeof(float) * 3 * (size_t)width * (size_t)height;
     if (r->d_frame) (void)hipFree(r->d_frame);
+    ring_free(r);
     if (r->d_accum) (void)hipFree(r->d_accum);
     if (r->d_display) (void)hipFree(r->d_display);
     if (r->d_part) (void)hipFree(r->d_part);
@@ -787,6 +900,7 @@ int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count) {
         PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     }
     r->n_lights = count;
+    r->lights_version++;  // new contents, possibly in the same array: the render-ahead ring is stale
     return PT_OK;
 }
 
@@ -822,10 +936,10 @@ int pt_render(pt_renderer* r, float* host_rgb) {
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     r->frame_id++;  // :623
     size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
-    PT_HIP(hipMemsetAsync(r->d_frame, 0, bytes, r->stream), "hipMemset frame");
-    int rc = launch_frames(r, r->d_frame, r->frame_id, 1);
+    const float* img = nullptr;
+    int rc = render_frame_image(r, &img);
     if (rc) return rc;
-    PT_HIP(hipMemcpyAsync(host_rgb, r->d_frame, bytes, hipMemcpyDeviceToHost, r->stream), "download frame");
+    PT_HIP(hipMemcpyAsync(host_rgb, img, bytes, hipMemcpyDeviceToHost, r->stream), "download frame");
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     return collect_pending(r);
 }
@@ -889,13 +1003,13 @@ int pt_display_add_frame(pt_renderer* r, int32_t* samples) {
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     r->frame_id++;  // Render: OptixRenderer.cpp:623
     const size_t n = 3 * (size_t)r->width * (size_t)r->height;
-    PT_HIP(hipMemsetAsync(r->d_frame, 0, sizeof(float) * n, r->stream), "hipMemset frame");
-    int rc = launch_frames(r, r->d_frame, r->frame_id, 1);
+    const float* img = nullptr;
+    int rc = render_frame_image(r, &img);
     if (rc) return rc;
     r->display_samples++;  // OptixView.cpp:239-248
     const bool continuous = r->display_max < 0;
     const float w = continuous ? 1.0f / (float)r->display_samples : 1.0f / (float)r->display_max;
-    PT_HIP(display_blend(r->d_display, r->d_frame, n, w, continuous, r->stream), "display blend");
+    PT_HIP(display_blend(r->d_display, img, n, w, continuous, r->stream), "display blend");
     if (samples) *samples = r->display_samples;
     return PT_OK;
 }
@@ -1114,6 +1228,15 @@ int pt_stats_reset(pt_renderer* r) {
     r->launches = 0;
     r->trace_ms = 0.0;
     r->trace_launches = 0;
+    return PT_OK;
+}
+
+int pt_set_render_ahead(pt_renderer* r, int32_t frames) {
+    if (!r || frames < 1 || frames > 1024) return fail(PT_ERR_INVALID, "pt_set_render_ahead: frames must be 1..1024");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+    ring_free(r);
+    r->render_ahead = frames;
     return PT_OK;
 }
 

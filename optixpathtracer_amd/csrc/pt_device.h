@@ -98,6 +98,9 @@ struct DevLaunch {
     float* accum;                    // W*H*3 fp32 sum
     double* accum64;                 // pt_set_accum_fp64: W*H*3 fp64 sum (accum then holds its
                                      // fp32 rounding); NULL = fp32 accumulation
+    size_t frame_stride;             // 0: the frames add into accum; else frame f of the launch is
+                                     // written alone to accum + f * frame_stride (pt_render's
+                                     // render-ahead ring, wavefront k_accum only)
     unsigned long long* counters;    // [0] segments [1] nodes visited [2] triangle tests [3] rays
     // debug path (pt_set_debug_pixel; the reference's isDebugRay, devicePrograms.cu:637-644):
     // the path of pixel debug_pixel (W*y + x, -1 = off) at frame debug_frame records every

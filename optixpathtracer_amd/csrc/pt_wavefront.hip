@@ -1062,6 +1062,16 @@ __global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L, int 
     const int P = L.width * L.height;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
         const size_t idx = (size_t)p * 3;
+        if (L.frame_stride) {  // render-ahead: each frame its own 1-spp image, a one-frame sum into zeros
+            for (int f = 0; f < nf; ++f) {
+                const float4 l = W.L[(size_t)f * P + p];
+                float* o = L.accum + (size_t)f * L.frame_stride + idx;
+                o[0] = 0.0f + l.x;
+                o[1] = 0.0f + l.y;
+                o[2] = 0.0f + l.z;
+            }
+            continue;
+        }
         if (L.accum64) {  // pt_set_accum_fp64: the frames' fp32 radiance summed in fp64
             double sx = L.accum64[idx], sy = L.accum64[idx + 1], sz = L.accum64[idx + 2];
             for (int f = 0; f < nf; ++f) {

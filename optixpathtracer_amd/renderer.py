@@ -168,6 +168,10 @@ class OptixRenderer:
     def set_kernel(self, kernel: int) -> None:
         check(self.lib.pt_set_kernel(self.h, int(kernel)), "pt_set_kernel")
 
+    def set_render_ahead(self, frames: int) -> None:
+        """pt_set_render_ahead: frames Render() may render ahead of the caller (1 = off)."""
+        check(self.lib.pt_set_render_ahead(self.h, int(frames)), "pt_set_render_ahead")
+
     def set_frames_per_launch(self, frames: int) -> None:
         check(self.lib.pt_set_frames_per_launch(self.h, int(frames)), "pt_set_frames_per_launch")
 

@@ -1,8 +1,8 @@
 set -e
-O=gpurun_out/r03zl
+O=gpurun_out/r03zm
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-tail -2 $O/smoke.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_render_ahead.py tests/test_gpu_parity.py tests/test_gpu_display.py -x -q --timeout 200 --timeout-method thread > $O/test_ra.log 2>&1 || { tail -40 $O/test_ra.log; exit 1; }
+tail -1 $O/test_ra.log
 timeout -k 10 300 python3 bench.py > $O/bench_default.json 2> $O/bench_default.log
-cat $O/bench_default.json
+python3 -c "import json; d=json.load(open('$O/bench_default.json')); print(d['value'], d['value_reference_loop'], d['reference_loop'], d['roofline']['vmem_pmc'], d['roofline']['pmc_stale'])"
