@@ -102,9 +102,10 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="override the config's scaling (all configs: strong = the step's spp in total, split "
                          "over the ranks; weak = the step's spp per rank)")
-    ap.add_argument("--reference-loops", type=int, default=256,
+    ap.add_argument("--reference-loops", type=int, default=1024,
                     help="pt_render calls (1 spp each, frame.id++, 24.9 MB download per call: the reference's "
-                         "OptixView::DrawOptix -> OptixRenderer::Render loop) timed for value_reference_loop; 0 = off")
+                         "OptixView::DrawOptix -> OptixRenderer::Render loop, here the 1024 samples of the "
+                         "configs[1] image) timed for value_reference_loop; 0 = off")
     a = ap.parse_args()
     scene, spp, scaling, a.workload = CONFIGS[a.config]
     a.scaling = a.scaling or scaling
@@ -420,14 +421,18 @@ def main():
             # allocated host array every call; the GL upload and blend are not part of it.
             # pt_render renders ahead (pt_set_render_ahead, default 64 frames: while the render state
             # is unchanged, a call that misses renders the next 1, 2, 4, ... 64 frame ids in one batch
-            # and later calls download theirs), so the loop is timed from a state change on, ramp
-            # included; the same loop with render-ahead off is reported beside it.
+            # and later calls download theirs; once at 64, the first call served from a batch also
+            # enqueues the next 64 frame ids, rendered while the caller downloads), so the loop is
+            # timed from a state change on, ramp included, and up to the end of the last look-ahead
+            # batch (frames no call asked for count as time, not as samples); the same loop with
+            # render-ahead off is reported beside it.
             def ref_loop(calls):
                 r.frame_id = 0
                 r.Render()  # the first call after a change renders its own frame only
                 t = time.perf_counter()
                 for _ in range(calls):
                     r.Render(np.empty((args.height, args.width, 3), np.float32))
+                r.synchronize()
                 return time.perf_counter() - t
 
             fid = r.frame_id

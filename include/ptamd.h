@@ -214,8 +214,11 @@ int pt_render(pt_renderer* r, float* host_rgb);
  * same between calls, a call whose frame id is not ready renders the next k frame ids as one
  * batch into a ring of k 1-spp images, k doubling on each such call that continues the sequence
  * (1, 2, 4, ... up to `frames`) and restarting at 1 after any change; later calls download their
- * frame from the ring.  Every image is bit-identical to rendering its frame alone; the ring holds
- * `frames` W*H*3 floats.  Out of device memory it falls back to one frame per call. */
+ * frame from the ring.  Once k reaches `frames`, the first pt_render served from a batch also
+ * enqueues the following `frames` frame ids into a second ring, which the GPU renders while the
+ * caller downloads the current batch (pt_render copies on a stream of its own).  Every image is
+ * bit-identical to rendering its frame alone; the two rings hold 2 * `frames` W*H*3 floats.  Out of
+ * device memory it falls back to one ring, then to one frame per call. */
 int pt_set_render_ahead(pt_renderer* r, int32_t frames);
 
 /* Device-resident accumulation (replaces the per-spp download + GL blend of

@@ -151,10 +151,21 @@ struct pt_renderer {
         }
     };
     int render_ahead = 64;
-    float* d_ring = nullptr;
-    int ring_cap = 0, ring_k = 1;
-    uint32_t ring_first = 0, ring_n = 0;
-    RenderKey ring_key;
+    // Two ring slots: once the ramp reaches render_ahead frames, pt_render enqueues the next
+    // batch into the other slot while the caller downloads this one's frames (on dl_stream,
+    // after the slot's `ready` event), so rendering and the device-to-host copies overlap.
+    struct RingSlot {
+        float* d = nullptr;
+        int cap = 0;
+        uint32_t first = 0, n = 0;
+        RenderKey key;
+        hipEvent_t ready = nullptr;  // recorded on `stream` after the slot's batch
+    };
+    RingSlot ring[2];
+    int ring_k = 1, ring_last = 0;  // ramp length, slot rendered last
+    bool spec_pending = false;      // a look-ahead batch was enqueued since the last collect
+    hipStream_t dl_stream = nullptr;
+    hipEvent_t ev_frame = nullptr;  // after the d_frame render (no ring)
     uint32_t lights_version = 0;
     float* d_display = nullptr;  // progressive view buffer (pt_display_*)
     int display_max = -1;
@@ -222,6 +233,7 @@ int collect_pending(pt_renderer* r) {
     size_t n = 0, tn = 0;
     PT_HIP(r->ev.collect(&sum, &n), "frame events");
     PT_HIP(r->tev.collect(&tsum, &tn), "trace-kernel events");
+    r->spec_pending = false;  // ev.collect waited for every enqueued batch
     r->launches += n;
     r->last_ms = sum;
     r->total_ms += sum;
@@ -409,56 +421,99 @@ pt_renderer::RenderKey render_key(const pt_renderer* r) {
 }
 
 void ring_free(pt_renderer* r) {
-    if (r->d_ring) (void)hipFree(r->d_ring);
-    r->d_ring = nullptr;
-    r->ring_cap = 0;
-    r->ring_n = 0;
+    for (pt_renderer::RingSlot& s : r->ring) {
+        if (s.d) (void)hipFree(s.d);  // hipFree waits for the work that may still read it
+        s.d = nullptr;
+        s.cap = 0;
+        s.n = 0;
+    }
     r->ring_k = 1;
 }
 
+// Slot s of the ring with room for `cap` frames and its ready event; false when the memory is not
+// there (the caller decides whether that is an error).
+int ring_reserve(pt_renderer* r, int s, int cap, size_t n3) {
+    pt_renderer::RingSlot& sl = r->ring[s];
+    if (!sl.ready) PT_HIP(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming), "hipEventCreate");
+    if (cap <= sl.cap) return PT_OK;
+    if (sl.d) {
+        PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
+        (void)hipFree(sl.d);
+        sl.d = nullptr;
+        sl.cap = 0;
+    }
+    const hipError_t e = hipMalloc(&sl.d, sizeof(float) * n3 * (size_t)cap);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc render-ahead ring");
+    sl.cap = cap;
+    return PT_OK;
+}
+
+// Render frames [first, first + n) into ring slot s as 1-spp images and record its ready event.
+int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t first, int n, size_t n3) {
+    pt_renderer::RingSlot& sl = r->ring[s];
+    sl.n = 0;
+    int rc = ring_reserve(r, s, n == 1 ? 1 : r->render_ahead, n3);  // one frame first, then the whole ring
+    if (rc == PT_OK) rc = launch_frames(r, sl.d, first, (uint32_t)n, nullptr, n3);
+    if (rc != PT_OK) return rc;
+    PT_HIP(hipEventRecord(sl.ready, r->stream), "hipEventRecord");
+    sl.key = k;
+    sl.first = first;
+    sl.n = (uint32_t)n;
+    return PT_OK;
+}
+
 // The 1-spp image of frame r->frame_id for pt_render / pt_display_add_frame (OptixRenderer::Render,
-// OptixRenderer.cpp:617-647), enqueued on r->stream.  With render-ahead (wavefront kernel), a frame
-// the ring holds under the same render state is taken from it; a miss renders the next k frames
-// as one batch into the ring, k doubling on every miss that continues the ring's frame sequence
-// under the same state (up to r->render_ahead) and 1 otherwise, so an interactive caller that
-// changes the camera every frame pays for one frame per call.  Each ring image is the one-frame
-// sum into zeros that the plain path computes, bit for bit.
-int render_frame_image(pt_renderer* r, const float** img) {
+// OptixRenderer.cpp:617-647), enqueued on r->stream; *ready (if given) is an event after which the
+// image may be read from another stream.  With render-ahead (wavefront kernel), a frame a ring
+// slot holds under the same render state is taken from it; a miss renders the next k frames as one
+// batch into a slot, k doubling on every miss that continues the ring's frame sequence under the
+// same state (up to r->render_ahead) and 1 otherwise, so an interactive caller that changes the
+// camera every frame pays for one frame per call.  With `look_ahead` (pt_render, whose downloads
+// run on dl_stream), the first call served from a full-length slot also enqueues the following
+// render_ahead frames into the other slot, which the GPU renders while the caller downloads this
+// slot's frames.  Each ring image is the one-frame sum into zeros that the plain path computes,
+// bit for bit.
+int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nullptr, bool look_ahead = false) {
     const size_t n3 = 3 * (size_t)r->width * (size_t)r->height;
     const int kernel = r->kernel == PT_KERNEL_AUTO ? PT_KERNEL_WAVEFRONT : r->kernel;
     const uint32_t f = r->frame_id;
     if (r->render_ahead > 1 && kernel == PT_KERNEL_WAVEFRONT) {
         const pt_renderer::RenderKey k = render_key(r);
-        const bool same = r->ring_n > 0 && k == r->ring_key;
-        if (same && f - r->ring_first < r->ring_n) {  // unsigned: also false for f < ring_first
-            *img = r->d_ring + (size_t)(f - r->ring_first) * n3;
-            return PT_OK;
+        int s = -1;
+        bool seq = false;
+        for (int i = 0; i < 2; ++i) {
+            const pt_renderer::RingSlot& sl = r->ring[i];
+            if (sl.n == 0 || !(k == sl.key)) continue;
+            if (f - sl.first < sl.n) s = i;  // unsigned: also false for f < first
+            if (i == r->ring_last && f == sl.first + sl.n) seq = true;
         }
-        const bool seq = same && f == r->ring_first + r->ring_n;
-        const int kf = seq ? std::min(2 * r->ring_k, r->render_ahead) : 1;
-        r->ring_n = 0;
         int rc = PT_OK;
-        if (kf > r->ring_cap) {  // one frame first, then the whole ring
-            const int cap = kf == 1 ? 1 : r->render_ahead;
-            if (r->d_ring) {
-                PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
-                (void)hipFree(r->d_ring);
-                r->d_ring = nullptr;
-                r->ring_cap = 0;
+        if (s < 0) {  // miss: the next k frames into the slot not rendered last
+            const int kf = seq ? std::min(2 * r->ring_k, r->render_ahead) : 1;
+            s = r->ring_last ^ 1;
+            rc = ring_fill(r, s, k, f, kf, n3);
+            if (rc == PT_OK) {
+                r->ring_k = kf;
+                r->ring_last = s;
             }
-            const hipError_t e = hipMalloc(&r->d_ring, sizeof(float) * n3 * (size_t)cap);
-            if (e == hipSuccess)
-                r->ring_cap = cap;
-            else
-                rc = hip_fail(e, "hipMalloc render-ahead ring");
         }
-        if (rc == PT_OK) rc = launch_frames(r, r->d_ring, f, (uint32_t)kf, nullptr, n3);
         if (rc == PT_OK) {
-            r->ring_key = k;
-            r->ring_first = f;
-            r->ring_n = (uint32_t)kf;
-            r->ring_k = kf;
-            *img = r->d_ring;
+            const pt_renderer::RingSlot& sl = r->ring[s];
+            *img = sl.d + (size_t)(f - sl.first) * n3;
+            if (ready) *ready = sl.ready;
+            const int o = s ^ 1;
+            const uint32_t next = sl.first + sl.n;
+            const bool debug = r->d_debug && r->debug_pixel >= 0;  // its records stay tied to the call
+            if (look_ahead && !debug && f == sl.first && (int)sl.n == r->render_ahead && r->ring_k == r->render_ahead &&
+                !(r->ring[o].n > 0 && r->ring[o].key == k && r->ring[o].first == next)) {
+                const int lrc = ring_fill(r, o, k, next, r->render_ahead, n3);
+                if (lrc == PT_OK) {
+                    r->ring_last = o;
+                    r->spec_pending = true;
+                } else if (lrc != PT_ERR_NOMEM) {
+                    return lrc;
+                }  // no room for the second slot: this call's frame is served all the same
+            }
             return PT_OK;
         }
         if (rc != PT_ERR_NOMEM) return rc;
@@ -470,6 +525,11 @@ int render_frame_image(pt_renderer* r, const float** img) {
     const int rc = launch_frames(r, r->d_frame, f, 1);
     if (rc) return rc;
     *img = r->d_frame;
+    if (ready) {
+        if (!r->ev_frame) PT_HIP(hipEventCreateWithFlags(&r->ev_frame, hipEventDisableTiming), "hipEventCreate");
+        PT_HIP(hipEventRecord(r->ev_frame, r->stream), "hipEventRecord");
+        *ready = r->ev_frame;
+    }
     return PT_OK;
 }
 
@@ -810,8 +870,9 @@ int pt_destroy(pt_renderer* r) {
         if (r->xstream[k]) (void)hipStreamDestroy(r->xstream[k]);
         if (r->ev_join[k]) (void)hipEventDestroy(r->ev_join[k]);
     }
-    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1]})
+    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1], r->ring[0].ready, r->ring[1].ready, r->ev_frame})
         if (e) (void)hipEventDestroy(e);
+    if (r->dl_stream) (void)hipStreamDestroy(r->dl_stream);
     r->ev.destroy();
     r->tev.destroy();
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -937,11 +998,18 @@ int pt_render(pt_renderer* r, float* host_rgb) {
     r->frame_id++;  // :623
     size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
     const float* img = nullptr;
-    int rc = render_frame_image(r, &img);
+    hipEvent_t ready = nullptr;
+    int rc = render_frame_image(r, &img, &ready, true);
     if (rc) return rc;
-    PT_HIP(hipMemcpyAsync(host_rgb, img, bytes, hipMemcpyDeviceToHost, r->stream), "download frame");
-    PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
-    return collect_pending(r);
+    // the download runs on its own stream after the image's event, so a look-ahead batch that
+    // render_frame_image enqueued on r->stream keeps rendering while this frame is copied
+    if (!r->dl_stream) PT_HIP(hipStreamCreateWithFlags(&r->dl_stream, hipStreamNonBlocking), "hipStreamCreate");
+    PT_HIP(hipStreamWaitEvent(r->dl_stream, ready, 0), "hipStreamWaitEvent");
+    PT_HIP(hipMemcpyAsync(host_rgb, img, bytes, hipMemcpyDeviceToHost, r->dl_stream), "download frame");
+    PT_HIP(hipStreamSynchronize(r->dl_stream), "hipStreamSynchronize");
+    // with a look-ahead batch in flight the launch events are retired later (pt_get_stats, a
+    // synchronising call, or launch_frames' kMaxPendingEvents bound), not by waiting for it here
+    return r->spec_pending ? PT_OK : collect_pending(r);
 }
 
 int pt_launch(pt_renderer* r, const pt_launch_params* lp) {

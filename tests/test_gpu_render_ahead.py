@@ -81,6 +81,30 @@ def test_render_ahead_matches_frame_by_frame(mode):
         r.close()
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["lambert", "dielectric"])
+def test_look_ahead_long_sequence(mode):
+    """Past the ramp (1+2+...+64 frames) pt_render serves from one ring slot while the next 64
+    frame ids render into the other (look-ahead, downloads on their own stream).  300 sequential
+    calls cross four look-ahead batches; then a camera move in the middle of a slot (the batch in
+    flight is discarded), a second long run, a jump back into the older slot and stats."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("layered")
+    a, b = _pair(sc, mode)
+    _same_calls(a, b, 300)
+    for r in (a, b):
+        r.SetCameraBlender(np.asarray(sc.camera_blender_pos, np.float32) + np.float32(0.03), sc.camera_blender_rot,
+                           sc.fov_deg)
+    _same_calls(a, b, 200)
+    back = a.frame_id - 70  # into the slot before the current one, if still held
+    for r in (a, b):
+        r.frame_id = back
+    _same_calls(a, b, 80)
+    assert a.stats()["samples"] >= b.stats()["samples"]
+    for r in (a, b):
+        r.close()
+
+
 def test_render_ahead_display_path():
     """pt_display_add_frame takes its frames from the same ring: the progressive view after 20
     frames is identical with and without render-ahead."""
