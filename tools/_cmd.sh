@@ -1,9 +1,9 @@
 set -e
-O=gpurun_out/r03zt
+O=gpurun_out/r03zu
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for a in "128 64" "128 32" "128 22" "128 16" "256 64" "256 43" "256 32" "512 64" "1024 64"; do
-  set -- $a
-  timeout -k 10 200 python3 bench.py --spp $1 --frames-per-launch $2 --no-cpu-baseline --reference-loops 0 --no-dedup-check --steps 5 > $O/b_$1_$2.json 2> $O/b_$1_$2.log
-  python3 -c "import json; d=json.load(open('$O/b_$1_$2.json')); print('$1 $2', d['value'], d['ms_per_step'])"
-done
+SECONDS=0; timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -3 $O/smoke.log; echo "smoke $SECONDS s"; SECONDS=0
+timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.log
+echo "bench $SECONDS s"
+python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['value_reference_loop'], d['mse_vs_oracle']['mse'])"
