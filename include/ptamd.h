@@ -251,7 +251,10 @@ int pt_accum_download64(pt_renderer* r, double* host_rgb);
 
 /* Waits for every device of the renderer. */
 int pt_synchronize(pt_renderer* r);
-void* pt_stream(pt_renderer* r);   /* hipStream_t of the library (of device_list[0]) */
+/* hipStream_t of the library (of device_list[0]).  After pt_render returns, a look-ahead batch
+ * (pt_set_render_ahead) may still be running on it: work a caller enqueues on this stream runs
+ * after that batch; pt_synchronize waits for it. */
+void* pt_stream(pt_renderer* r);
 /* Devices of a multi-device renderer (1 for a single-device one); ordinals into devices[]
  * (at most max entries). */
 int32_t pt_device_count(const pt_renderer* r);
