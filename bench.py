@@ -17,13 +17,17 @@ more step with 1024 frames per rank reports the weak-scaling rate as `value_weak
 `--config 3|4d|4l|5` runs BASELINE.json's other configs through the same harness (4d/4l: 4096
 spp per step); the driver's default run is configs[1].
 
-Extra fields: `roofline` (HBM roofline of the dominant kernels, the wavefront's trace kernels
-k_extend + k_trace_pair: 48 algorithmic bytes per traced ray, ray read + result write, over
-their per-launch average measured with one HIP event pair per launch on the library stream;
-`pipeline_gbps` is SURVEY.md §8(d)'s whole-path 396 B/segment + 12 B/sample over the render
-time; `traffic` is the PMC HBM bytes per launch from profiles/traffic.json) and
-`cpu_baseline` (the CPU oracle, oracle/, timed on a bounded band of the same workload on the
-host cores, rank 0 at N=1 only).
+Extra fields: `roofline` (HBM roofline of the mode's dominant kernel, measured with one HIP event
+pair per launch on the stream it runs on: in the Lambert / Conductor / Dielectric modes the
+wavefront's trace kernels k_extend + k_trace_pair, 48 algorithmic bytes per traced ray, ray read +
+result write, with `vmem` -- the same launches against the CU vector-memory path that binds them,
+16-B lane loads from global memory per second against one line per CU-cycle; in the Default /
+Layered modes k_shade_nee, the layered NEE eval, 216 algorithmic bytes per item, with `valu` -- its
+VALU issue fraction from a committed PMC summary; `pipeline_gbps` is SURVEY.md §8(d)'s whole-path
+396 B/segment + 12 B/sample over the render time; `traffic` is the PMC HBM bytes per launch from
+profiles/traffic.json), `cpu_baseline` (the CPU oracle, oracle/, timed on a bounded band of the
+same workload on the host cores, rank 0 at N=1 only) and `distributed` (the process group's
+backend and rank count and the reduce time per step).
 """
 from __future__ import annotations
 
@@ -41,6 +45,18 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table
 BYTES_PER_SEGMENT = 396  # compulsory SoA queue + gather traffic per path segment
 BYTES_PER_SAMPLE = 12  # final fp32 RGB accumulate
 BYTES_PER_TRACE = 48  # trace-kernel share per ray: ray record read 32 B + hit / result write 16 B
+# k_shade_nee per NEE item: queue entry 4 + hit record 16 + ray direction 16 + triangle gathers
+# (isect v0 16 + shade 64) + material 32 + throughput|seed 16 + light index 4 + radiance RMW 32 +
+# seed write-back 16 (pt_wavefront.hip k_shade_nee)
+BYTES_PER_NEE_ITEM = 4 + 16 + 16 + 80 + 32 + 16 + 4 + 32 + 16
+CLOCK_HZ = 2.4e9  # MI355X shader clock (MI355X_MICROARCH.md; tools/td_probe.hip measured at 2400 MHz)
+N_CUS, N_SIMDS = 256, 1024
+# tools/td_probe.hip (profiles/r03s_td_probe.json): a 16-B-per-lane load costs the CU's texture
+# data path about one cycle per distinct cache line its lanes touch (64 lines: 65 cycles), so the
+# vector-memory ceiling for scattered 16-B loads is one lane load per CU-cycle
+VMEM_LOADS_PER_S = N_CUS * CLOCK_HZ
+NODE_LOADS = 7  # 16-B loads per global BVH4 node visit (6 sign-selected planes + child links)
+TRI_LOADS = 3   # per triangle test (v0 | index, e1 | material, e2)
 
 
 # BASELINE.json configs by index: scene, spp per step, scaling, workload label.  The default
@@ -74,6 +90,14 @@ def pmc_record(path: Path, sources_sha: str):
     except Exception:
         return None, False
     return d, d.get("sources_sha") == sources_sha
+
+
+def device_identity(torch, dev: int) -> dict:
+    """Which GPU the numbers came from (name, gfx arch, CUs, memory), for attributing outliers."""
+    p = torch.cuda.get_device_properties(dev)
+    return {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
+            "memory_gb": round(p.total_memory / 2**30, 1),
+            "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")}
 
 
 def parse():
@@ -185,6 +209,8 @@ def main():
 
     from optixpathtracer_amd import sharding
 
+    reduce_s = []  # per timed step (sharding.render_step)
+
     def step(s: int, scaling: str | None = None):
         if (scaling or args.scaling) == "strong":  # args.spp frames per step in total, split over the ranks
             first, n = sharding.split_frames(args.spp, rank, world, base=1 + s * args.spp)
@@ -192,7 +218,7 @@ def main():
             first, n = sharding.frame_range(s, rank, world, args.spp)
         # clear -> render -> sync -> RCCL reduce over xGMI -> sync torch's stream (the next
         # step's clear runs on libptamd's stream and must not overtake the reduce)
-        sharding.render_step(r, accum, dist, first, n)
+        return sharding.render_step(r, accum, dist, first, n)
 
     for s in range(args.warmup):
         step(s)
@@ -205,7 +231,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(args.warmup + s)
+        reduce_s.append(step(args.warmup + s))
         if rank == 0:
             log(f"[bench] step {s + 1}/{args.steps} {time.perf_counter() - t0:.2f}s")
     torch.cuda.synchronize(dev)
@@ -218,6 +244,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    distributed = sharding.distributed_report(dist, reduce_s, accum)  # a collective at N > 1
     per_step_spp = args.spp if args.scaling == "strong" else args.spp * world
     samples_total = args.width * args.height * per_step_spp * args.steps
     value = samples_total / elapsed / 1e6
@@ -282,22 +309,79 @@ def main():
             ach1 = s1["trace_kernel_bytes"] / l1 / (ms1 / 1e3) / 1e9
             single = {"value": round(args.width * args.height * per_step_spp / e2 / 1e6, 3),
                       "avg_launch_ms": round(ms1, 4), "achieved": round(ach1, 2),
-                      "frac": round(ach1 / HBM_PEAK_GBPS, 5), "launches": l1}
+                      "frac": round(ach1 / HBM_PEAK_GBPS, 5), "launches": l1,
+                      "shade_avg_launch_ms": round(s1["shade_kernel_ms"] / max(1, s1["shade_kernel_launches"]), 4),
+                      "shade_items_per_launch": s1["shade_kernel_items"] / max(1, s1["shade_kernel_launches"])}
         r.set_wavefront_streams(args.wavefront_streams)
+    # One more untimed render of two 64-frame batches with the traversal counters on (a separate
+    # kernel instance): node visits (global / from LDS), triangle tests and rays per trace launch,
+    # for the vector-memory roofline of the trace kernels (roofline.vmem).  Its time is not used.
+    trav = None
+    if args.kernel != 0:
+        r.set_traversal_stats(True)
+        r.stats_reset()
+        r.accum_clear()
+        r.render_frames(1, min(args.spp, 2 * args.frames_per_launch))
+        trav = r.stats()
+        r.set_traversal_stats(False)
     if rank == 0:
         nan_px = int(np.isnan(img).any(axis=-1).sum())
         kernel_s = st["total_render_ms"] / 1e3
         alg_bytes = st["segments"] * BYTES_PER_SEGMENT + st["samples"] * BYTES_PER_SAMPLE
+        fused = scene.material_mode in (1, 2, 3)
+        vmem_line = valu_line = trace_line = None
         if st["trace_kernel_launches"] > 0:
-            # wavefront: the dominant kernels are the trace kernels (k_extend for bounce 0,
-            # k_trace_pair = shadow rays of bounce b + extension rays of b+1), each launch
-            # bracketed by its own HIP event pair on the library stream
-            dom = "k_extend+k_trace_pair"
             launches = int(st["trace_kernel_launches"])
+            t_bytes = st["trace_kernel_bytes"] / launches
+            t_s = st["trace_kernel_ms"] / 1e3 / launches
+            trace_line = {"kernel": "k_extend+k_trace_pair" if fused else "k_extend", "launches": launches,
+                          "avg_launch_ms": round(t_s * 1e3, 4), "bytes_per_launch": int(t_bytes),
+                          "achieved": round(t_bytes / t_s / 1e9, 2), "frac": round(t_bytes / t_s / 1e9 / HBM_PEAK_GBPS, 5)}
+            if trav and trav["trace_kernel_launches"] > 0:
+                # 16-B lane loads of global memory per trace launch, counted like trace_kernel_bytes:
+                # 7 per global node visit, 3 per triangle test, 2 per extension-ray record and 3 per
+                # shadow-ray record (record loads are coalesced, 8 lanes per line, so as line touches
+                # they count up to 8x; they are 6 % of the loads)
+                tl = int(trav["trace_kernel_launches"])
+                g_nodes = trav["nodes_visited"] - trav["lds_nodes_visited"]
+                ext_rays = trav["rays"] - trav["shadow_rays"]
+                loads = (NODE_LOADS * g_nodes + TRI_LOADS * trav["tri_tests"] + 2 * ext_rays
+                         + 3 * trav["shadow_rays"]) / tl
+                ach_v = loads / t_s
+                vmem_line = {
+                    "unit": "16-B lane loads/s", "lane_loads_per_launch": round(loads),
+                    "achieved": round(ach_v / 1e9, 2), "ceiling": round(VMEM_LOADS_PER_S / 1e9, 1),
+                    "frac": round(ach_v / VMEM_LOADS_PER_S, 4),
+                    "ceiling_def": "1 line per CU-cycle x 256 CUs x 2.4 GHz (tools/td_probe.hip)",
+                    "node_visits_per_ray": round(trav["nodes_visited"] / max(1, trav["rays"]), 3),
+                    "lds_node_share": round(trav["lds_nodes_visited"] / max(1, trav["nodes_visited"]), 4),
+                    "tri_tests_per_ray": round(trav["tri_tests"] / max(1, trav["rays"]), 3),
+                    "node_lane_utilisation": round(trav["nodes_visited"] / max(1, 64 * trav["wave_node_steps"]), 4),
+                }
+                if single:
+                    sv = loads / (single["avg_launch_ms"] / 1e3)
+                    vmem_line["single_stream"] = {"achieved": round(sv / 1e9, 2), "frac": round(sv / VMEM_LOADS_PER_S, 4)}
+        if fused and trace_line:
+            # Lambert / Conductor / Dielectric: the trace kernels are the dominant kernels (k_extend
+            # at bounce 0, k_trace_pair = shadow rays of bounce b + extension rays of b+1), each
+            # launch bracketed by its own HIP event pair on the stream it runs on
+            dom = trace_line["kernel"]
+            launches = trace_line["launches"]
             per_launch_bytes = st["trace_kernel_bytes"] / launches
             avg_launch_s = st["trace_kernel_ms"] / 1e3 / launches
-            bytes_def = ("32 B ray record read per traced ray + 16 B per hit / shadow record written "
-                         "(k_extend writes its hit to every frame copy of the batch)")
+            bytes_def = ("48 B per traced ray: the 32-B ray record read and one 16-B result, the hit record of an "
+                         "extension ray (one per pixel at bounce 0, shared by the pixel's frames of the batch) or "
+                         "the deferred radiance add of an unoccluded shadow ray")
+        elif st["shade_kernel_launches"] > 0:
+            # Default / Layered: k_shade_nee (the stochastic layered NEE eval) takes 53-60 % of a frame
+            # (DESIGN.md §8); its bound is VALU issue (roofline.valu), its HBM figure is reported too
+            dom = "k_shade_nee"
+            launches = int(st["shade_kernel_launches"])
+            per_launch_bytes = st["shade_kernel_items"] * BYTES_PER_NEE_ITEM / launches
+            avg_launch_s = st["shade_kernel_ms"] / 1e3 / launches
+            bytes_def = (f"{BYTES_PER_NEE_ITEM} B per NEE item: queue entry, hit record, ray direction, triangle "
+                         "gathers (v0 + shading record), material, throughput|seed, light index, radiance "
+                         "read-modify-write, seed write-back")
         else:
             dom = "k_render_mega"
             launches = max(1, int(st["kernel_launches"]))
@@ -322,7 +406,7 @@ def main():
                 pmc_stale["traffic"] = {**fig, "sources_sha": tjd.get("sources_sha"), "stale": True}
         valu = None  # the VALU fraction beside the HBM roofline, from PMC passes
         vd, cur = pmc_record(ROOT / "profiles" / "valu.json", sha)
-        if vd and dom == "k_extend+k_trace_pair" and args.config == "2":
+        if vd and fused and args.config == "2":
             fig = {k: vd.get(k) for k in ("kernel", "valu_busy", "valu_issue_slots", "lane_utilisation", "wait_per_wave_cycle")}
             if cur:
                 valu = {**fig, "sources_sha": sha}
@@ -330,7 +414,7 @@ def main():
                 pmc_stale["valu_pmc"] = {**fig, "sources_sha": vd.get("sources_sha"), "stale": True}
         vmem = None  # the vector memory path (TA / TD busy), what the trace kernel waits on
         md, cur = pmc_record(ROOT / "profiles" / "vmem.json", sha)
-        if md and dom == "k_extend+k_trace_pair" and args.config == "2":
+        if md and fused and args.config == "2":
             fig = {k: md.get(k) for k in ("kernel", "ta_busy", "td_busy", "td_tc_stall", "l2_read_latency_cycles")}
             if cur:
                 vmem = {**fig, "sources_sha": sha}
@@ -338,7 +422,7 @@ def main():
                 pmc_stale["vmem_pmc"] = {**fig, "sources_sha": md.get("sources_sha"), "stale": True}
         shade = None  # the memory-bound kernel of a Lambert frame, PMC HBM GB/s (tools/shade_pmc.py)
         sd, cur = pmc_record(ROOT / "profiles" / "shade_pmc.json", sha)
-        if sd and dom == "k_extend+k_trace_pair" and args.config == "2":
+        if sd and fused and args.config == "2":
             ks = sd.get("kernels", {})
             # bounces >= 1 (the bounce-0 instance derives its path state, shade0)
             sk = ks.get("k_shade_fused<1, false, false>") or ks.get("k_shade_fused<1, false>")
@@ -348,6 +432,22 @@ def main():
                     shade = {**fig, "sources_sha": sha}
                 else:
                     pmc_stale["shade_pmc"] = {**fig, "sources_sha": sd.get("sources_sha"), "stale": True}
+        if dom == "k_shade_nee":
+            # VALU issue of k_shade_nee (tools/pmc.sh + tools/pmc_summary.py --shade-json, per config):
+            # wave64 VALU instructions x 2 cycles (MI355X_MICROARCH.md: a SIMD issues one every 2
+            # cycles with several waves) over 1024 SIMDs x clock x the single-stream launch time
+            nd, cur = pmc_record(ROOT / "profiles" / f"shade_valu_config{args.config}.json", sha)
+            if nd:
+                t_launch = (single or {}).get("shade_avg_launch_ms") or avg_launch_s * 1e3
+                insts = nd.get("valu_insts_per_dispatch")
+                fig = {"kernel": nd.get("kernel"), "valu_insts_per_dispatch": insts,
+                       "lane_utilisation": nd.get("lane_utilisation"), "launch_ms": round(t_launch, 4),
+                       "issue_frac": round(insts * 2 / (N_SIMDS * CLOCK_HZ * t_launch / 1e3), 4) if insts else None,
+                       "issue_def": "wave64 VALU insts x 2 cycles / (1024 SIMDs x 2.4 GHz x single-stream launch time)"}
+                if cur:
+                    valu_line = {**fig, "sources_sha": sha}
+                else:
+                    pmc_stale["valu"] = {**fig, "sources_sha": nd.get("sources_sha"), "stale": True}
         out = {
             "metric": "Msamples/sec at 1920x1080, max-depth 8; MSE vs reference",
             "value": round(value, 3),
@@ -404,6 +504,13 @@ def main():
                 # whose address / data units are near saturation (vmem_pmc), not VALU issue (valu_pmc)
                 "valu_pmc": valu,
                 "vmem_pmc": vmem,
+                # the unit that binds the trace kernels: 16-B lane loads through the CU's vector
+                # memory path against one line per CU-cycle
+                "vmem": vmem_line,
+                # k_shade_nee (Default / Layered): VALU issue fraction
+                "valu": valu_line,
+                # the trace kernels' own line when they are not the dominant kernel (Default / Layered)
+                "trace": trace_line if not fused else None,
                 # PMC HBM bandwidth of the shading kernel (2 x FETCH_SIZE + WRITE_SIZE per launch)
                 "shade_pmc": shade,
                 "single_stream": single,
@@ -413,6 +520,9 @@ def main():
                 "pmc_stale": pmc_stale or None,
             },
             "image": {"mean": float(np.nanmean(img) / per_step_spp), "nan_pixels": nan_px},
+            # what the process group ran: backend ("nccl" = RCCL), ranks, reduce time per step
+            "distributed": distributed,
+            "device": device_identity(torch, local_rank),
         }
         if world == 1 and args.reference_loops > 0 and args.kernel != 0:
             # The reference's own call pattern (OptixView::DrawOptix -> OptixRenderer::Render,
@@ -437,6 +547,25 @@ def main():
 
             fid = r.frame_id
             e4 = ref_loop(args.reference_loops)
+            # Latency of a state change in the steady state: after 200 sequential
+            # calls (a look-ahead batch in flight), the camera moves and one call is timed: it waits
+            # for the batch already enqueued (bounded by pt_set_render_ahead_budget), then renders
+            # and downloads its own frame.  Median of 3.
+            import statistics
+
+            lat = []
+            for k in range(3):
+                r.SetCameraBlender(scene.camera_blender_pos, scene.camera_blender_rot, scene.fov_deg)
+                r.frame_id = 0
+                for _ in range(200):
+                    r.Render(np.empty((args.height, args.width, 3), np.float32))
+                pos = np.asarray(scene.camera_blender_pos, np.float32) + np.float32(1e-3 * (k + 1))
+                r.SetCameraBlender(pos, scene.camera_blender_rot, scene.fov_deg)
+                t = time.perf_counter()
+                r.Render(np.empty((args.height, args.width, 3), np.float32))
+                lat.append(time.perf_counter() - t)
+            r.SetCameraBlender(scene.camera_blender_pos, scene.camera_blender_rot, scene.fov_deg)
+            r.synchronize()
             r.set_render_ahead(1)
             n_off = min(args.reference_loops, 64)
             e5 = ref_loop(n_off)
@@ -446,6 +575,8 @@ def main():
             out["reference_loop"] = {"calls": args.reference_loops, "ms_per_call": round(e4 / args.reference_loops * 1e3, 3),
                                      "what": "pt_render: 1 spp per call, frame.id++, D2H download of the 24.9 MB "
                                              "frame per call (the reference's DrawOptix loop), render-ahead on",
+                                     "first_call_after_change_ms": round(1e3 * statistics.median(lat), 3),
+                                     "render_ahead_budget_ms": 50.0,
                                      "no_render_ahead": {"calls": n_off, "ms_per_call": round(e5 / n_off * 1e3, 3),
                                                          "value": round(args.width * args.height * n_off / e5 / 1e6, 3)}}
         if world == 1 and not args.no_cpu_baseline:

@@ -136,6 +136,22 @@ typedef struct pt_stats {
     uint64_t wave_node_steps;
     uint64_t wave_tri_steps;
     uint64_t wave_refills;
+    /* node visits of the wavefront trace kernels served from the top BVH levels staged in LDS
+       (counted while pt_set_traversal_stats(r, 1)); nodes_visited - lds_nodes_visited loaded
+       their 128-B node from global memory */
+    uint64_t lds_nodes_visited;
+    /* the bounce's dominant shading kernel of the wavefront path (k_shade_fused / k_shade0_pixel
+       in the Lambert, Conductor and Dielectric modes; k_shade_nee, the layered NEE eval, in the
+       Default and Layered modes), timed like the trace kernels while pt_set_kernel_timing(r, 1) */
+    double shade_kernel_ms;
+    uint64_t shade_kernel_launches;
+    uint64_t shade_kernel_items; /* their queue items (hit records shaded; NEE items), always counted */
+    /* render-ahead (pt_set_render_ahead): frames rendered into the ring, and pt_render /
+       pt_display_add_frame calls served from it.  samples, segments and the kernel counters
+       include every rendered frame, also those rendered ahead that no call has asked for yet
+       (frames_rendered_ahead - frames_served_ahead of them at most). */
+    uint64_t frames_rendered_ahead;
+    uint64_t frames_served_ahead;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;
@@ -210,16 +226,24 @@ int pt_launch(pt_renderer* r, const pt_launch_params* params);
  * the first pt_resize (as :621). */
 int pt_render(pt_renderer* r, float* host_rgb);
 /* Render-ahead for pt_render / pt_display_add_frame (wavefront kernel; default 64 frames, 1 = off).
- * While the size, camera, lights, max bounces, material mode, kernel and debug pixel stay the
- * same between calls, a call whose frame id is not ready renders the next k frame ids as one
- * batch into a ring of k 1-spp images, k doubling on each such call that continues the sequence
- * (1, 2, 4, ... up to `frames`) and restarting at 1 after any change; later calls download their
- * frame from the ring.  Once k reaches `frames`, the first pt_render served from a batch also
- * enqueues the following `frames` frame ids into a second ring, which the GPU renders while the
- * caller downloads the current batch (pt_render copies on a stream of its own).  Every image is
- * bit-identical to rendering its frame alone; the two rings hold 2 * `frames` W*H*3 floats.  Out of
- * device memory it falls back to one ring, then to one frame per call. */
+ * While the size, camera, lights, max bounces, material mode and kernel stay the same between
+ * calls, a call whose frame id is not ready renders the next k frame ids as one batch into a ring
+ * of 1-spp images, k doubling on each such call that continues the sequence (1, 2, 4, ...) and
+ * restarting at 1 after any change; later calls download their frame from the ring.  Once k
+ * reaches its target, the first pt_render served from a batch also enqueues the following k frame
+ * ids into a second ring, which the GPU renders while the caller downloads the current batch
+ * (pt_render copies on a stream of its own).  The target is the smallest of `frames`, a memory
+ * cap and a time budget: a batch's wavefront queues (208 B per path) and the two rings (2 * k
+ * W*H*3 floats) take at most a quarter of the device memory and no more than is free, and a
+ * batch's estimated duration (from the last measured ring batch) stays within
+ * pt_set_render_ahead_budget (default 50 ms) -- the most a call that changes the state waits
+ * for work already enqueued.  At 1080p 64 frames hold about 31 GB.  Every image is bit-identical
+ * to rendering its frame alone.  A batch that does not fit in device memory lowers the cap for
+ * the rest of the sequence, and the call renders its own frame alone.  With a debug pixel set
+ * (pt_set_debug_pixel) every call renders its own frame, so the records belong to that call. */
 int pt_set_render_ahead(pt_renderer* r, int32_t frames);
+/* Upper bound, in ms of estimated GPU time, on one render-ahead batch (default 50; 0 = none). */
+int pt_set_render_ahead_budget(pt_renderer* r, float max_ms);
 
 /* Device-resident accumulation (replaces the per-spp download + GL blend of
  * Renderer/OptixView.cpp:201-255 / AddPathtracedFrame.frag:18-24).  Renders frame ids

@@ -125,6 +125,12 @@ class pt_stats(C.Structure):
         ("wave_node_steps", C.c_uint64),
         ("wave_tri_steps", C.c_uint64),
         ("wave_refills", C.c_uint64),
+        ("lds_nodes_visited", C.c_uint64),
+        ("shade_kernel_ms", C.c_double),
+        ("shade_kernel_launches", C.c_uint64),
+        ("shade_kernel_items", C.c_uint64),
+        ("frames_rendered_ahead", C.c_uint64),
+        ("frames_served_ahead", C.c_uint64),
     ]
 
 
@@ -163,6 +169,7 @@ SIGNATURES = {
     "pt_set_kernel": (C.c_int, [_R, C.c_int32]),
     "pt_set_frames_per_launch": (C.c_int, [_R, C.c_int32]),
     "pt_set_render_ahead": (C.c_int, [_R, C.c_int32]),
+    "pt_set_render_ahead_budget": (C.c_int, [_R, C.c_float]),
     "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel_timing": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),

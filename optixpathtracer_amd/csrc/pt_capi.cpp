@@ -87,7 +87,8 @@ struct EventPool {
 
 // Device counters: [0] segments [1] nodes visited [2] triangle tests [3] rays [4] stack
 // overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces
-// [9..13] wave schedule of the trace kernels (pt_stats wave_*).
+// [9..13] wave schedule of the trace kernels (pt_stats wave_*) [14] node visits served from LDS
+// [15] items of the timed shading kernel (pt_stats shade_kernel_items).
 constexpr int kCounters = 16;
 // event pairs held by one renderer before launch_frames retires them (EventPool)
 constexpr size_t kMaxPendingEvents = 4096;
@@ -141,25 +142,34 @@ struct pt_renderer {
     // frame ids download them from the ring
     struct RenderKey {
         int w = 0, h = 0, n_lights = 0, max_bounces = 0, mode = 0, kernel = 0, debug_pixel = -1;
-        uint32_t lights_version = 0, debug_frame = 0;
+        uint32_t lights_version = 0, debug_frame = 0, debug_version = 0;
         const void* lights = nullptr;
         float cam[3 + 16 + 16] = {};
         bool operator==(const RenderKey& o) const {
             return w == o.w && h == o.h && n_lights == o.n_lights && max_bounces == o.max_bounces && mode == o.mode &&
                    kernel == o.kernel && debug_pixel == o.debug_pixel && lights_version == o.lights_version &&
-                   debug_frame == o.debug_frame && lights == o.lights && std::memcmp(cam, o.cam, sizeof cam) == 0;
+                   debug_frame == o.debug_frame && debug_version == o.debug_version && lights == o.lights &&
+                   std::memcmp(cam, o.cam, sizeof cam) == 0;
         }
     };
     int render_ahead = 64;
-    // Two ring slots: once the ramp reaches render_ahead frames, pt_render enqueues the next
-    // batch into the other slot while the caller downloads this one's frames (on dl_stream,
-    // after the slot's `ready` event), so rendering and the device-to-host copies overlap.
+    // A render-ahead batch is also bounded by memory and by time (ahead_frames): its queues and
+    // the two ring slots take at most a quarter of the device memory (and only what is free), and
+    // its estimated duration stays within ahead_budget_ms (pt_set_render_ahead_budget), so a
+    // call that changes the state waits for at most about that much work already enqueued.
+    double ahead_budget_ms = 50.0;
+    double frame_ms_est = 0.0;  // ms per frame of the last measured ring batch (0: none yet)
+    int ahead_oom_cap = 1 << 30;  // largest batch since an allocation failed (reset per sequence)
+    // Two ring slots: once the ramp reaches its length, pt_render enqueues the next batch into
+    // the other slot while the caller downloads this one's frames (on dl_stream, after the
+    // slot's `ready` event), so rendering and the device-to-host copies overlap.
     struct RingSlot {
         float* d = nullptr;
         int cap = 0;
         uint32_t first = 0, n = 0;
         RenderKey key;
-        hipEvent_t ready = nullptr;  // recorded on `stream` after the slot's batch
+        hipEvent_t start = nullptr, ready = nullptr;  // recorded on `stream` around the slot's batch
+        bool measured = true;                         // its duration is in frame_ms_est
     };
     RingSlot ring[2];
     int ring_k = 1, ring_last = 0;  // ramp length, slot rendered last
@@ -167,6 +177,7 @@ struct pt_renderer {
     hipStream_t dl_stream = nullptr;
     hipEvent_t ev_frame = nullptr;  // after the d_frame render (no ring)
     uint32_t lights_version = 0;
+    uint32_t debug_version = 0;  // bumped by pt_set_debug_pixel (the records are rewritten)
     float* d_display = nullptr;  // progressive view buffer (pt_display_*)
     int display_max = -1;
     int display_samples = 0;
@@ -181,9 +192,16 @@ struct pt_renderer {
     bool kernel_timing = false;
     bool primary_dedup = true;  // pt_set_primary_dedup
     EventPool tev;
-    std::vector<hipEvent_t> tev_frame;  // 2 * max_bounces events handed to one frame
+    std::vector<hipEvent_t> tev_frame;  // 2 * (max_bounces + 1) events handed to one frame
     double trace_ms = 0.0;
     uint64_t trace_launches = 0;
+    // the same for the dominant shading kernel of a bounce (pt_stats shade_kernel_*)
+    EventPool sev;
+    std::vector<hipEvent_t> sev_frame;
+    double shade_ms = 0.0;
+    uint64_t shade_launches = 0;
+    // render-ahead frames rendered into the ring and calls served from it (pt_stats)
+    uint64_t ahead_rendered = 0, ahead_served = 0;
     bool pending = false;
     uint64_t samples = 0;
     double last_ms = 0.0, total_ms = 0.0;
@@ -218,8 +236,6 @@ struct pt_renderer {
         S.n_nodes = bvh_nodes;
         S.lds_nodes = nullptr;
         S.n_lds = 0;
-        S.n_mats = std::max(1, nmesh);
-        S.mat_lds = 0;
         return S;
     }
     float* accum() const { return user_accum ? user_accum : d_accum; }
@@ -229,16 +245,19 @@ namespace {
 
 int collect_pending(pt_renderer* r) {
     if (!r->pending) return PT_OK;
-    double sum = 0.0, tsum = 0.0;
-    size_t n = 0, tn = 0;
+    double sum = 0.0, tsum = 0.0, ssum = 0.0;
+    size_t n = 0, tn = 0, sn = 0;
     PT_HIP(r->ev.collect(&sum, &n), "frame events");
     PT_HIP(r->tev.collect(&tsum, &tn), "trace-kernel events");
+    PT_HIP(r->sev.collect(&ssum, &sn), "shading-kernel events");
     r->spec_pending = false;  // ev.collect waited for every enqueued batch
     r->launches += n;
     r->last_ms = sum;
     r->total_ms += sum;
     r->trace_ms += tsum;
     r->trace_launches += tn;
+    r->shade_ms += ssum;
+    r->shade_launches += sn;
     r->pending = false;
     return PT_OK;
 }
@@ -281,7 +300,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
     // callers that never synchronise through the library (pt_stream interop, device sum buffers,
     // loops over pt_launch / pt_display_add_frame) would grow the event pools without bound:
     // past kMaxPendingEvents pairs, retire them first (this waits for the enqueued work)
-    if (r->ev.used + r->tev.used > kMaxPendingEvents && (rc = collect_pending(r)) != PT_OK) return rc;
+    if (r->ev.used + r->tev.used + r->sev.used > kMaxPendingEvents && (rc = collect_pending(r)) != PT_OK) return rc;
     const DevScene S = r->scene();
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
@@ -357,20 +376,26 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                 if (rc) return rc;
             }
             const hipEvent_t* tev = nullptr;
+            const hipEvent_t* sev = nullptr;
             if (r->kernel_timing) {
                 r->tev_frame.resize(2 * (size_t)(r->max_bounces + 1));  // <= max_bounces + 1 trace launches
                 for (int k = 0; k <= r->max_bounces; ++k)
                     PT_HIP(r->tev.next(&r->tev_frame[2 * k], &r->tev_frame[2 * k + 1]), "hipEventCreate");
                 tev = r->tev_frame.data();
+                r->sev_frame.resize(2 * (size_t)(r->max_bounces + 1));  // <= max_bounces shading launches
+                for (int k = 0; k <= r->max_bounces; ++k)
+                    PT_HIP(r->sev.next(&r->sev_frame[2 * k], &r->sev_frame[2 * k + 1]), "hipEventCreate");
+                sev = r->sev_frame.data();
             }
             if (!dual) PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
-            int n_timed = 0;
+            int n_timed = 0, n_stimed = 0;
             PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, sk ? r->xwf[sk] : r->wf, first + f,
                                           nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
                                           dual && batch > 0 ? r->ev_accum[(batch - 1) & 1] : nullptr,
-                                          dual ? r->ev_accum[batch & 1] : nullptr),
+                                          dual ? r->ev_accum[batch & 1] : nullptr, sev, &n_stimed),
                    "wavefront launch");
             if (tev) r->tev.give_back((size_t)(r->max_bounces + 1 - n_timed));  // pairs never recorded
+            if (sev) r->sev.give_back((size_t)(r->max_bounces + 1 - n_stimed));
             if (!dual) PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
             f += (uint32_t)nf;
         }
@@ -413,6 +438,7 @@ pt_renderer::RenderKey render_key(const pt_renderer* r) {
     k.debug_pixel = r->d_debug ? r->debug_pixel : -1;
     k.debug_frame = r->debug_frame;
     k.lights_version = r->lights_version;
+    k.debug_version = r->debug_version;
     k.lights = r->d_lights;
     std::memcpy(k.cam, r->cam_pos, sizeof r->cam_pos);
     std::memcpy(k.cam + 3, r->inv_view, sizeof r->inv_view);
@@ -426,15 +452,52 @@ void ring_free(pt_renderer* r) {
         s.d = nullptr;
         s.cap = 0;
         s.n = 0;
+        s.measured = true;
     }
     r->ring_k = 1;
+    r->ahead_oom_cap = 1 << 30;
 }
 
-// Slot s of the ring with room for `cap` frames and its ready event; false when the memory is not
-// there (the caller decides whether that is an error).
+// Frames one render-ahead batch may hold now.  Memory: the batch's wavefront queues (one stream)
+// and both ring slots take at most a quarter of the device memory, and no more than is free
+// besides what the renderer already holds for them (render-ahead sized its queues
+// like pt_render_frames, 28 GB at 1080p).  Time: the batch's estimated duration stays within
+// ahead_budget_ms, from the per-frame time of the last measured ring batch (a call that changes
+// the state waits behind at most the batch in flight).  Always >= 1.
+int ahead_frames(pt_renderer* r, size_t n3, bool by_time) {
+    int k = std::min(r->render_ahead, r->ahead_oom_cap);
+    const size_t P = n3 / 3;
+    const size_t per_frame = wavefront_bytes((int)P, std::max(1, r->max_bounces)) + 2 * sizeof(float) * n3;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b > 0) {
+        size_t held = 2 * sizeof(float) * n3 * (size_t)std::max(r->ring[0].cap, r->ring[1].cap);
+        if (r->wf.paths > 0) held += wavefront_bytes(r->wf.paths, r->wf.max_bounces);
+        const size_t avail = std::min(total_b / 4, free_b + held);
+        k = std::min<size_t>((size_t)k, std::max<size_t>(1, avail / per_frame));
+    } else {
+        (void)hipGetLastError();
+    }
+    if (by_time && r->ahead_budget_ms > 0.0 && r->frame_ms_est > 0.0)
+        k = std::min(k, std::max(1, (int)(r->ahead_budget_ms / r->frame_ms_est)));
+    return std::max(1, k);
+}
+
+// A finished ring batch's duration per frame -> frame_ms_est (no wait: only batches done by now).
+void ring_measure(pt_renderer* r) {
+    for (pt_renderer::RingSlot& sl : r->ring) {
+        if (sl.measured || sl.n == 0 || hipEventQuery(sl.ready) != hipSuccess) continue;
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, sl.start, sl.ready) == hipSuccess && ms > 0.0f) r->frame_ms_est = ms / sl.n;
+        (void)hipGetLastError();
+        sl.measured = true;
+    }
+}
+
+// Slot s of the ring with room for `cap` frames and its events.
 int ring_reserve(pt_renderer* r, int s, int cap, size_t n3) {
     pt_renderer::RingSlot& sl = r->ring[s];
-    if (!sl.ready) PT_HIP(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming), "hipEventCreate");
+    if (!sl.ready) PT_HIP(hipEventCreate(&sl.ready), "hipEventCreate");
+    if (!sl.start) PT_HIP(hipEventCreate(&sl.start), "hipEventCreate");
     if (cap <= sl.cap) return PT_OK;
     if (sl.d) {
         PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
@@ -443,22 +506,30 @@ int ring_reserve(pt_renderer* r, int s, int cap, size_t n3) {
         sl.cap = 0;
     }
     const hipError_t e = hipMalloc(&sl.d, sizeof(float) * n3 * (size_t)cap);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc render-ahead ring");
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // a later launch's hipGetLastError must not see this failure
+        return hip_fail(e, "hipMalloc render-ahead ring");
+    }
     sl.cap = cap;
     return PT_OK;
 }
 
-// Render frames [first, first + n) into ring slot s as 1-spp images and record its ready event.
-int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t first, int n, size_t n3) {
+// Render frames [first, first + n) into ring slot s (room for `cap` frames) as 1-spp images and
+// record its events.
+int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t first, int n, int cap, size_t n3) {
     pt_renderer::RingSlot& sl = r->ring[s];
     sl.n = 0;
-    int rc = ring_reserve(r, s, n == 1 ? 1 : r->render_ahead, n3);  // one frame first, then the whole ring
+    sl.measured = true;
+    int rc = ring_reserve(r, s, std::max(n, cap), n3);
+    if (rc == PT_OK) PT_HIP(hipEventRecord(sl.start, r->stream), "hipEventRecord");
     if (rc == PT_OK) rc = launch_frames(r, sl.d, first, (uint32_t)n, nullptr, n3);
     if (rc != PT_OK) return rc;
     PT_HIP(hipEventRecord(sl.ready, r->stream), "hipEventRecord");
     sl.key = k;
     sl.first = first;
     sl.n = (uint32_t)n;
+    sl.measured = false;
+    r->ahead_rendered += (uint64_t)n;
     return PT_OK;
 }
 
@@ -467,17 +538,21 @@ int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t f
 // image may be read from another stream.  With render-ahead (wavefront kernel), a frame a ring
 // slot holds under the same render state is taken from it; a miss renders the next k frames as one
 // batch into a slot, k doubling on every miss that continues the ring's frame sequence under the
-// same state (up to r->render_ahead) and 1 otherwise, so an interactive caller that changes the
-// camera every frame pays for one frame per call.  With `look_ahead` (pt_render, whose downloads
-// run on dl_stream), the first call served from a full-length slot also enqueues the following
-// render_ahead frames into the other slot, which the GPU renders while the caller downloads this
-// slot's frames.  Each ring image is the one-frame sum into zeros that the plain path computes,
-// bit for bit.
+// same state (up to ahead_frames: render_ahead, the memory cap and the time budget) and 1
+// otherwise, so an interactive caller that changes the camera every frame pays for one frame per
+// call.  With `look_ahead` (pt_render, whose downloads run on dl_stream), the first call served
+// from a slot of the full ramp length also enqueues the following frames into the other slot,
+// which the GPU renders while the caller downloads this slot's frames.  Each ring image is the
+// one-frame sum into zeros that the plain path computes, bit for bit.  The debug pixel's records
+// belong to the call that renders its frame, so with a debug pixel set every call renders its
+// own frame.
 int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nullptr, bool look_ahead = false) {
     const size_t n3 = 3 * (size_t)r->width * (size_t)r->height;
     const int kernel = r->kernel == PT_KERNEL_AUTO ? PT_KERNEL_WAVEFRONT : r->kernel;
     const uint32_t f = r->frame_id;
-    if (r->render_ahead > 1 && kernel == PT_KERNEL_WAVEFRONT) {
+    const bool debug = r->d_debug && r->debug_pixel >= 0;
+    if (r->render_ahead > 1 && kernel == PT_KERNEL_WAVEFRONT && !debug) {
+        ring_measure(r);
         const pt_renderer::RenderKey k = render_key(r);
         int s = -1;
         bool seq = false;
@@ -489,37 +564,46 @@ int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nu
         }
         int rc = PT_OK;
         if (s < 0) {  // miss: the next k frames into the slot not rendered last
-            const int kf = seq ? std::min(2 * r->ring_k, r->render_ahead) : 1;
+            if (!seq) r->ahead_oom_cap = 1 << 30;  // a new sequence tries the full length again
+            const int kmax = ahead_frames(r, n3, false);
+            const int kf = seq ? std::min(2 * r->ring_k, ahead_frames(r, n3, true)) : 1;
             s = r->ring_last ^ 1;
-            rc = ring_fill(r, s, k, f, kf, n3);
+            rc = ring_fill(r, s, k, f, kf, kf == 1 ? 1 : kmax, n3);
             if (rc == PT_OK) {
                 r->ring_k = kf;
                 r->ring_last = s;
+            } else if (rc == PT_ERR_NOMEM) {
+                // no room for this batch: later batches of the sequence stay below it, and this
+                // call renders its own frame alone (below)
+                r->ahead_oom_cap = std::max(1, kf / 2);
+                r->ring[s].n = 0;
             }
         }
         if (rc == PT_OK) {
             const pt_renderer::RingSlot& sl = r->ring[s];
             *img = sl.d + (size_t)(f - sl.first) * n3;
             if (ready) *ready = sl.ready;
+            r->ahead_served++;
             const int o = s ^ 1;
             const uint32_t next = sl.first + sl.n;
-            const bool debug = r->d_debug && r->debug_pixel >= 0;  // its records stay tied to the call
-            if (look_ahead && !debug && f == sl.first && (int)sl.n == r->render_ahead && r->ring_k == r->render_ahead &&
+            const int kl = ahead_frames(r, n3, true);  // the full ramp length now
+            // the ramp is done once doubling this slot's length would pass the target length
+            if (look_ahead && f == sl.first && sl.n > 1 && 2 * (int)sl.n > kl &&
                 !(r->ring[o].n > 0 && r->ring[o].key == k && r->ring[o].first == next)) {
-                const int lrc = ring_fill(r, o, k, next, r->render_ahead, n3);
+                const int lrc = ring_fill(r, o, k, next, kl, ahead_frames(r, n3, false), n3);
                 if (lrc == PT_OK) {
+                    r->ring_k = kl;
                     r->ring_last = o;
                     r->spec_pending = true;
                 } else if (lrc != PT_ERR_NOMEM) {
                     return lrc;
+                } else {
+                    r->ring[o].n = 0;
                 }  // no room for the second slot: this call's frame is served all the same
             }
             return PT_OK;
         }
         if (rc != PT_ERR_NOMEM) return rc;
-        // no room for the ring or its k-frame queues: render frame by frame from here on
-        ring_free(r);
-        r->render_ahead = 1;
     }
     PT_HIP(hipMemsetAsync(r->d_frame, 0, sizeof(float) * n3, r->stream), "hipMemset frame");
     const int rc = launch_frames(r, r->d_frame, f, 1);
@@ -870,11 +954,13 @@ int pt_destroy(pt_renderer* r) {
         if (r->xstream[k]) (void)hipStreamDestroy(r->xstream[k]);
         if (r->ev_join[k]) (void)hipEventDestroy(r->ev_join[k]);
     }
-    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1], r->ring[0].ready, r->ring[1].ready, r->ev_frame})
+    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1], r->ring[0].ready, r->ring[1].ready,
+                         r->ring[0].start, r->ring[1].start, r->ev_frame})
         if (e) (void)hipEventDestroy(e);
     if (r->dl_stream) (void)hipStreamDestroy(r->dl_stream);
     r->ev.destroy();
     r->tev.destroy();
+    r->sev.destroy();
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
     return PT_OK;
@@ -1257,6 +1343,12 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->wave_node_steps = c[11];
     out->wave_tri_steps = c[12];
     out->wave_refills = c[13];
+    out->lds_nodes_visited = c[14];
+    out->shade_kernel_ms = r->shade_ms;
+    out->shade_kernel_launches = r->shade_launches;
+    out->shade_kernel_items = c[15];
+    out->frames_rendered_ahead = r->ahead_rendered;
+    out->frames_served_ahead = r->ahead_served;
     // a multi-device renderer reports the work of all its devices (times are device 0's)
     for (pt_renderer* p : r->peers) {
         pt_stats ps;
@@ -1273,6 +1365,8 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
         out->wave_node_steps += ps.wave_node_steps;
         out->wave_tri_steps += ps.wave_tri_steps;
         out->wave_refills += ps.wave_refills;
+        out->lds_nodes_visited += ps.lds_nodes_visited;
+        out->shade_kernel_items += ps.shade_kernel_items;
         out->shadow_rays += ps.shadow_rays;
         out->trace_kernel_rays += ps.trace_kernel_rays;
         out->trace_kernel_bytes += ps.trace_kernel_bytes;
@@ -1296,6 +1390,9 @@ int pt_stats_reset(pt_renderer* r) {
     r->launches = 0;
     r->trace_ms = 0.0;
     r->trace_launches = 0;
+    r->shade_ms = 0.0;
+    r->shade_launches = 0;
+    r->ahead_rendered = r->ahead_served = 0;
     return PT_OK;
 }
 
@@ -1305,6 +1402,12 @@ int pt_set_render_ahead(pt_renderer* r, int32_t frames) {
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     ring_free(r);
     r->render_ahead = frames;
+    return PT_OK;
+}
+
+int pt_set_render_ahead_budget(pt_renderer* r, float max_ms) {
+    if (!r || !(max_ms >= 0.0f)) return fail(PT_ERR_INVALID, "pt_set_render_ahead_budget: max_ms must be >= 0");
+    r->ahead_budget_ms = max_ms;
     return PT_OK;
 }
 
@@ -1455,6 +1558,7 @@ extern "C" int pt_set_debug_pixel(pt_renderer* r, int32_t x, int32_t y, uint32_t
     PT_HIP(hipMemset(r->d_debug, 0, bytes), "hipMemset debug records");
     r->debug_pixel = r->width * y + x;
     r->debug_frame = frame_id;
+    r->debug_version++;  // records cleared: no ring image rendered before stands for this state
     return PT_OK;
 }
 

@@ -43,43 +43,12 @@ struct DevScene {
     // n_lds = 0 everywhere else
     const BNode4* lds_nodes;
     int n_lds;
-    int n_mats;   // meshes in the material table
-    // the material table is staged in the block's dynamic LDS (stage_mats, shading kernels);
-    // 0 everywhere else
-    int mat_lds;
 };
 
 // Material record (3 x float4 per mesh):
 //   [0] albedo.rgb | metallic     [1] roughness | has_normals | albedo_tex | normal_tex
 //   [2] metal_rough_tex | any texture | 0 | 0          (texture ids as int bits, -1 = none)
 constexpr int kMatStride = 3;
-
-// Per-block material table in LDS (north_star: "per-tile material params staged through LDS";
-// the reference reads them from the mesh's SBT record, MeshSBTData.h:6-28).  The shading kernels
-// launch with kMatStride * 16 B per mesh of dynamic LDS when the table has at most kMatLdsMax
-// meshes, copy it in once per block and read every hit's material from there
-// (PT_MAT_LDS; DESIGN.md §5 gives the A/B).
-#ifndef PT_MAT_LDS
-#define PT_MAT_LDS 0
-#endif
-constexpr int kMatLdsMax = 256;  // 12 KB
-extern __shared__ float4 pt_mat_lds[];
-__device__ __forceinline__ float4 mat_load(const DevScene& S, int k) {
-    if (PT_MAT_LDS && S.mat_lds) return pt_mat_lds[k];
-    return S.mats[k];
-}
-// Every thread of the block calls it (it synchronises the block) after any block-uniform exit.
-__device__ __forceinline__ void stage_mats(DevScene& S) {
-    if (!PT_MAT_LDS || S.n_mats > kMatLdsMax) return;
-    const int n = S.n_mats * kMatStride;
-    for (int i = (int)threadIdx.x; i < n; i += (int)blockDim.x) pt_mat_lds[i] = S.mats[i];
-    __syncthreads();
-    S.mat_lds = 1;
-}
-// dynamic LDS bytes a shading launch passes for stage_mats
-inline size_t mat_lds_bytes(int n_mats) {
-    return (PT_MAT_LDS && n_mats <= kMatLdsMax) ? sizeof(float4) * kMatStride * (size_t)n_mats : 0;
-}
 
 struct DevLight {
     float px, py, pz, cr, cg, cb;
@@ -149,6 +118,7 @@ __device__ __forceinline__ uint64_t probe_clock(const T& dep) {  // once `dep` i
 
 struct TravStats {
     uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0, retrace = 0;
+    uint32_t lds_nodes = 0;  // node visits served from the staged top levels (stage_top_nodes)
     // wave schedule (trace_range, lane 0 of each wave): iterations, active lanes summed over
     // them, iterations running the node half / the triangle half, refill blocks
     uint32_t steps = 0, active = 0, node_steps = 0, tri_steps = 0, refills = 0;
@@ -286,7 +256,7 @@ __device__ __forceinline__ void tri_texcoord(const DevScene& S, int ti, float u,
 // AlphaCutout: a hit on an albedo-textured mesh is ignored when the decoded alpha < 0.9
 // (__anyhit__radiance / __anyhit__shadow, devicePrograms.cu:545-561).
 __device__ __forceinline__ bool alpha_cut(const DevScene& S, int ti, int mi, float u, float v) {
-    const int at = __float_as_int(mat_load(S, kMatStride * mi + 1).z);
+    const int at = __float_as_int(S.mats[kMatStride * mi + 1].z);
     float x, y;
     tri_texcoord(S, ti, u, v, x, y);
     return tex_sample(S, at, x, y, true).w < 0.9f;
@@ -702,7 +672,10 @@ template <int ANY, bool STATS, int DEPTH>
 __device__ __forceinline__ bool trav_node_step(const DevScene& S, TravState& s, int* __restrict__ stk, int stride,
                                                int* spill, TravStats& ts) {
     if (s.cur >= 0) {
-        if (STATS) ts.nodes++;
+        if (STATS) {
+            ts.nodes++;
+            ts.lds_nodes += s.cur < S.n_lds;
+        }
         float t0, t1, t2, t3;
         int c0, c1, c2, c3;
         const NodeLoad nl = node_load(S, s, s.cur);
@@ -856,25 +829,17 @@ __device__ __forceinline__ void apply_textures(const DevScene& S, int ti, float 
 
 // TEX: the scene has textures (kernels are instantiated both ways so untextured scenes keep
 // the texture code out of their register budget).
-#ifndef PT_SHADE_EDGES
-#define PT_SHADE_EDGES 1
-#endif
 template <bool TEX>
 __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 d, SurfaceHit& s) {
     const int ti = h.tri;
     const float4 A = S.isect[3 * ti];
     const float4 S0 = S.shade[4 * ti], S1 = S.shade[4 * ti + 1], S2 = S.shade[4 * ti + 2], S3 = S.shade[4 * ti + 3];
-#if PT_SHADE_EDGES
     // the edges again from the vertices: e = v - v0 is the one fp32 subtraction k_gather stored in
     // isect, so Ng is bit-identical, and the hit costs five gathers instead of seven
     const float4 E1 = make_float4(S0.x - A.x, S0.y - A.y, S0.z - A.z, 0.0f);
     const float4 E2 = make_float4(S1.x - A.x, S1.y - A.y, S1.z - A.z, 0.0f);
     const int mi = __float_as_int(S3.w);
-#else
-    const float4 E1 = S.isect[3 * ti + 1], E2 = S.isect[3 * ti + 2];
-    const int mi = __float_as_int(E1.w);
-#endif
-    const float4 M0 = mat_load(S, kMatStride * mi), M1 = mat_load(S, kMatStride * mi + 1);
+    const float4 M0 = S.mats[kMatStride * mi], M1 = S.mats[kMatStride * mi + 1];
     f3 wo_w = normalize(-d);
     f3 v0 = mk(A.x, A.y, A.z), v1 = mk(S0.x, S0.y, S0.z), v2 = mk(S1.x, S1.y, S1.z);
     f3 n0 = mk(S0.w, S1.w, S2.x), n1 = mk(S2.y, S2.z, S2.w), n2 = mk(S3.x, S3.y, S3.z);
@@ -897,7 +862,7 @@ __device__ __forceinline__ void reconstruct(const DevScene& S, const Hit& h, f3 
     s.metallic = M0.w;
     s.roughness = M1.x;
     if (TEX) {
-        const float4 M2 = mat_load(S, kMatStride * mi + 2);
+        const float4 M2 = S.mats[kMatStride * mi + 2];
         if (M2.y != 0.0f) apply_textures(S, ti, u, v, M1, M2, s.albedo, s.metallic, s.roughness, Ns);
     }
     f3 c1 = cross(Ns, mk(0.0f, 0.0f, 1.0f));

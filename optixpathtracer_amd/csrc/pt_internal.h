@@ -63,7 +63,9 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces);
 void wavefront_free(WFState& W);
 // Enqueue one frame (all bounces) of the wavefront pipeline; adds the frame into L.accum.
 // trace_events (optional): up to 2 * (L.max_bounces + 1) events recorded around the trace
-// launches; *n_timed (optional) receives the number of event pairs recorded.
+// launches; *n_timed (optional) receives the number of event pairs recorded.  shade_events /
+// n_shade_timed: the same for the bounce's dominant shading kernel (k_shade_fused / k_shade0_pixel
+// in the fused modes, k_shade_nee in Default / Layered), up to 2 * L.max_bounces events.
 // nf frames (frame .. frame + nf - 1) are traced together; W must hold nf * W * H paths.
 // primary_dedup: trace the batch's identical camera rays once per pixel (k_extend `dup`).
 // accum_wait / accum_done (optional): the batch's k_accum waits for accum_wait and records
@@ -72,7 +74,8 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
                                   const hipEvent_t* trace_events,
                                   int* n_timed = nullptr, hipEvent_t accum_wait = nullptr,
-                                  hipEvent_t accum_done = nullptr);
+                                  hipEvent_t accum_done = nullptr, const hipEvent_t* shade_events = nullptr,
+                                  int* n_shade_timed = nullptr);
 
 // Render launches.
 hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,

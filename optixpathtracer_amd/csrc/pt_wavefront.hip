@@ -80,12 +80,13 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 }
 
 // Traversal statistics of a wave into the renderer's counters ([1] nodes, [2] triangle tests,
-// [3] rays, [4] stack overflows, [8] strict re-traces).
+// [3] rays, [4] stack overflows, [8] strict re-traces, [14] node visits served from LDS).
 template <bool STATS>
 __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, const TravStats& ts) {
     if (!STATS || !counters) return;
     const unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
     const unsigned long long e = wave_sum_u64(ts.overflow), r = wave_sum_u64(ts.retrace);
+    const unsigned long long l = wave_sum_u64(ts.lds_nodes);
     if (lane_id() == 0) {  // the wave-schedule counts are kept by every lane alike: lane 0's
         atomicAdd(&counters[1], a);
         atomicAdd(&counters[2], c);
@@ -97,6 +98,7 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
         atomicAdd(&counters[11], (unsigned long long)ts.node_steps);
         atomicAdd(&counters[12], (unsigned long long)ts.tri_steps);
         atomicAdd(&counters[13], (unsigned long long)ts.refills);
+        atomicAdd(&counters[14], l);
     }
 }
 
@@ -506,7 +508,6 @@ __device__ __forceinline__ int vis0_index(const DevLaunch& L, int path, int li) 
 
 template <bool TEX>
 __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunch L, WFState W) {
-    stage_mats(S);
     const int P1 = L.width * L.height;
     const int nl = L.n_lights;
     const int n = P1 * nl;
@@ -549,8 +550,8 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
     __shared__ int lds_sh[kWaves + 1], lds_q[kWaves + 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters) atomicAdd(&L.counters[15], (unsigned long long)n);
     if ((int)(blockIdx.x * kBlock) >= n) return;  // block-uniform
-    stage_mats(S);
     {
         const int i = (int)(blockIdx.x * kBlock + threadIdx.x);
         const bool valid = i < n;
@@ -659,8 +660,9 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
     constexpr int kBlock = shf_block(MODE), kWaves = kBlock / 64;
     const int P1 = L.width * L.height;
     __shared__ int lds_q[kWaves + 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters)
+        atomicAdd(&L.counters[15], (unsigned long long)P1 * (unsigned long long)nf);
     if ((int)(blockIdx.x * kBlock) >= P1) return;  // block-uniform
-    stage_mats(S);
     const int p = (int)(blockIdx.x * kBlock + threadIdx.x);
     const bool valid = p < P1;
     int tri = -1;
@@ -824,7 +826,6 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
     __shared__ int lds_sh[kWavesShA + 1];
     __shared__ int lds_nee[kShadeBuckets * (kWavesShA + 1)], lds_smp[kShadeBuckets * (kWavesShA + 1)];
     if ((int)(blockIdx.x * kBlockShA) >= n) return;  // block-uniform
-    stage_mats(S);
     const int i = (int)(blockIdx.x * kBlockShA + threadIdx.x);
     bool emit = false;
     int nee_bucket = -1, smp_bucket = -1, code = 0;
@@ -990,8 +991,9 @@ __device__ __forceinline__ int bucket_total(const WFState& W, int b, int c0) {
 // to W.beta before k_shade_smp reads it).
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene S, DevLaunch L, WFState W, int b) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters)
+        atomicAdd(&L.counters[15], (unsigned long long)bucket_total(W, b, kNee0));
     if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kNee0)) return;  // block-uniform
-    stage_mats(S);
     const int j = bucket_entry(W, W.nq, b, kNee0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
     if (j < 0) return;  // no barrier below
     const float4 hv = W.hit[j], c = W.ray_d[b & 1][j];
@@ -1028,7 +1030,6 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_smp(DevScene 
     constexpr int kW = kBlockShB / 64;
     __shared__ int lds_q[kW + 1];
     if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kSmp0)) return;  // block-uniform
-    stage_mats(S);
     const int j = bucket_entry(W, W.sq, b, kSmp0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
     bool emit_next = false;
     f3 o, d;
@@ -1138,25 +1139,24 @@ dim3 occupancy_grid(K kernel, int cus) {
 template <int MODE, bool TEX>
 hipError_t launch_shade_t(bool fused, const DevScene& S, const DevLaunch& L, const WFState& W, int b, int items,
                           hipStream_t stream, int phase, int vis0, int shade0) {
-    const size_t mlds = mat_lds_bytes(S.n_mats);
     if (fused) {
         if constexpr (MODE == kModeLambert || MODE == kModeConductor || MODE == kModeDielectric)
         {
             if (shade0)
-                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, true>), item_grid(items, shf_block(MODE)), dim3(shf_block(MODE)), mlds,
+                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, true>), item_grid(items, shf_block(MODE)), dim3(shf_block(MODE)), 0,
                                    stream, S, L, W, b, vis0);
             else
-                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, false>), item_grid(items, shf_block(MODE)), dim3(shf_block(MODE)), mlds,
+                hipLaunchKernelGGL((k_shade_fused<MODE, TEX, false>), item_grid(items, shf_block(MODE)), dim3(shf_block(MODE)), 0,
                                    stream, S, L, W, b, vis0);
         }
     } else if (phase == 0) {
-        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockShA), dim3(kBlockShA), mlds, stream, S, L, W, b,
+        hipLaunchKernelGGL((k_shade_a<MODE, TEX>), item_grid(items, kBlockShA), dim3(kBlockShA), 0, stream, S, L, W, b,
                            vis0);
     } else if (phase == 1) {
-        hipLaunchKernelGGL((k_shade_nee<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), mlds, stream, S, L,
+        hipLaunchKernelGGL((k_shade_nee<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L,
                            W, b);
     } else {
-        hipLaunchKernelGGL((k_shade_smp<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), mlds, stream, S, L,
+        hipLaunchKernelGGL((k_shade_smp<MODE, TEX>), item_grid(items, kBlockShB), dim3(kBlockShB), 0, stream, S, L,
                            W, b);
     }
     return hipGetLastError();
@@ -1174,9 +1174,9 @@ hipError_t launch_shade0_pixel_t(const DevScene& S, const DevLaunch& L, const WF
     constexpr int block = shf_block(MODE);
     const dim3 grid = item_grid(L.width * L.height, block);
     if (S.texinfo)
-        hipLaunchKernelGGL((k_shade0_pixel<MODE, true>), grid, dim3(block), mat_lds_bytes(S.n_mats), stream, S, L, W, nf);
+        hipLaunchKernelGGL((k_shade0_pixel<MODE, true>), grid, dim3(block), 0, stream, S, L, W, nf);
     else
-        hipLaunchKernelGGL((k_shade0_pixel<MODE, false>), grid, dim3(block), mat_lds_bytes(S.n_mats), stream, S, L, W,
+        hipLaunchKernelGGL((k_shade0_pixel<MODE, false>), grid, dim3(block), 0, stream, S, L, W,
                            nf);
     return hipGetLastError();
 }
@@ -1260,7 +1260,7 @@ void wavefront_free(WFState& W) {
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
                                   const hipEvent_t* trace_events, int* n_timed, hipEvent_t accum_wait,
-                                  hipEvent_t accum_done) {
+                                  hipEvent_t accum_done, const hipEvent_t* shade_events, int* n_shade_timed) {
     const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
     hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
@@ -1273,6 +1273,17 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     const bool fused = fused_mode(mode);
     const bool tex = S.texinfo != nullptr;  // textured scene: kernels with texture sampling
     int timed = 0;                          // trace launches bracketed by trace_events
+    int stimed = 0;                         // shading launches bracketed by shade_events
+    // the timed shading kernel of a bounce: k_shade_fused / k_shade0_pixel (fused modes), k_shade_nee
+    // (Default / Layered: the stochastic layered eval, 53-60 % of their frame)
+    auto shade_timed = [&](auto launch) -> hipError_t {
+        hipError_t r;
+        if (shade_events && (r = hipEventRecord(shade_events[2 * stimed], stream)) != hipSuccess) return r;
+        if ((r = launch()) != hipSuccess) return r;
+        if (shade_events && (r = hipEventRecord(shade_events[2 * stimed + 1], stream)) != hipSuccess) return r;
+        ++stimed;
+        return hipSuccess;
+    };
     auto extend = [&](int b, int dup, int copies) -> hipError_t {
         hipError_t r;
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
@@ -1333,11 +1344,11 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         if (!vis0) return hipSuccess;
         if (tex)
             hipLaunchKernelGGL(k_shadow0_setup<true>, item_grid(P1 * vis0, kBlockWF), dim3(kBlockWF),
-                               mat_lds_bytes(S.n_mats), stream, S, L,
+                               0, stream, S, L,
                                W);
         else
             hipLaunchKernelGGL(k_shadow0_setup<false>, item_grid(P1 * vis0, kBlockWF), dim3(kBlockWF),
-                               mat_lds_bytes(S.n_mats), stream, S,
+                               0, stream, S,
                                L, W);
         hipError_t r = hipGetLastError();
         if (r != hipSuccess || (r = shadow_vis(0, 1)) != hipSuccess) return r;
@@ -1354,9 +1365,12 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         if ((e = shadow0()) != hipSuccess) return e;
         for (int b = 0; b < maxb; ++b) {
             if (b == 0 && pixel0) {
-                if ((e = launch_shade0_pixel(mode, S, L, W, nf, stream)) != hipSuccess) return e;
-            } else if ((e = launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0, b == 0 && lean)) !=
-                       hipSuccess) {
+                if ((e = shade_timed([&] { return launch_shade0_pixel(mode, S, L, W, nf, stream); })) != hipSuccess)
+                    return e;
+            } else if ((e = shade_timed([&] {
+                            return launch_shade_mode(mode, true, S, L, W, b, P, stream, 0, b == 0 ? vis0 : 0,
+                                                     b == 0 && lean);
+                        })) != hipSuccess) {
                 return e;
             }
             if ((e = pair(b)) != hipSuccess) return e;
@@ -1371,7 +1385,9 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
             // or k_shadow_vis + k_nee_compact) get the NEE eval, the continuing ones the sample
             if ((e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 0, v0)) != hipSuccess) return e;
             if (!v0 && (e = shadow_vis(b, 0)) != hipSuccess) return e;
-            if ((e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 1, v0)) != hipSuccess) return e;
+            if ((e = shade_timed([&] { return launch_shade_mode(mode, false, S, L, W, b, P, stream, 1, v0); })) !=
+                hipSuccess)
+                return e;
             if (b + 1 < maxb && (e = launch_shade_mode(mode, false, S, L, W, b, P, stream, 2, v0)) != hipSuccess)
                 return e;
         }
@@ -1380,6 +1396,7 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
     if (accum_done && (e = hipEventRecord(accum_done, stream)) != hipSuccess) return e;
     if (n_timed) *n_timed = timed;  // fused modes: max_bounces + 1; Default / Layered: max_bounces
+    if (n_shade_timed) *n_shade_timed = stimed;  // max_bounces
     return hipGetLastError();
 }
 

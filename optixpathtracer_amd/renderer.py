@@ -172,6 +172,10 @@ class OptixRenderer:
         """pt_set_render_ahead: frames Render() may render ahead of the caller (1 = off)."""
         check(self.lib.pt_set_render_ahead(self.h, int(frames)), "pt_set_render_ahead")
 
+    def set_render_ahead_budget(self, max_ms: float) -> None:
+        """pt_set_render_ahead_budget: bound (ms of GPU time) on one render-ahead batch, 0 = none."""
+        check(self.lib.pt_set_render_ahead_budget(self.h, float(max_ms)), "pt_set_render_ahead_budget")
+
     def set_frames_per_launch(self, frames: int) -> None:
         check(self.lib.pt_set_frames_per_launch(self.h, int(frames)), "pt_set_frames_per_launch")
 
@@ -179,7 +183,8 @@ class OptixRenderer:
         check(self.lib.pt_set_traversal_stats(self.h, 1 if enable else 0), "pt_set_traversal_stats")
 
     def set_kernel_timing(self, enable: bool = True) -> None:
-        """Time every wavefront closest-hit trace launch with its own HIP event pair."""
+        """Time every wavefront trace launch and every launch of the bounce's dominant shading
+        kernel with its own HIP event pair (pt_stats trace_kernel_* / shade_kernel_*)."""
         check(self.lib.pt_set_kernel_timing(self.h, 1 if enable else 0), "pt_set_kernel_timing")
 
     # -- headless progressive view (OptixView accumulation on the device) -------------------

@@ -160,11 +160,14 @@ def _gpu_bench_worker(rank, world, port, spp, steps, out_dir):
     accum = torch.zeros((32, 48, 3), dtype=torch.float32, device=dev)
     torch.cuda.synchronize(dev)
     r.set_accum_device_buffer(accum.data_ptr())
+    red = []
     for s in range(steps):
         first, n = sharding.split_frames(spp, rank, world, base=1 + s * spp)
-        sharding.render_step(r, accum, dist, first, n)
+        red.append(sharding.render_step(r, accum, dist, first, n))
         if rank == 0:
             np.save(os.path.join(out_dir, f"step{s}.npy"), accum.cpu().numpy())
+    rep = sharding.distributed_report(dist, red, accum)
+    assert rep["backend"] == "gloo" and rep["world_size"] == world and rep["steps"] == steps
     dist.barrier()
     r.close()
     dist.destroy_process_group()
@@ -199,3 +202,65 @@ def test_two_process_bench_steps_device_accumulators(tmp_path):
         r.render_frames(1 + s * spp, spp)
         np.testing.assert_allclose(got, r.accum(), rtol=2e-6, atol=1e-7)
     r.close()
+
+
+class _NullRenderer:
+    """bench.py's renderer calls, with nothing rendered (the reporting path only)."""
+
+    def accum_clear(self):
+        pass
+
+    def render_frames(self, first, n):
+        pass
+
+    def synchronize(self):
+        pass
+
+
+def _report_worker(rank, world, port, out_dir):
+    sys.path.insert(0, str(ROOT))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from optixpathtracer_amd import sharding
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    accum = torch.full((8, 12, 3), float(rank + 1), dtype=torch.float32)
+    red = [sharding.render_step(_NullRenderer(), accum, dist, 1 + s, 1) for s in range(3)]
+    if rank == 1:
+        time.sleep(0.05)  # rank 1's own mean must not decide the max-over-ranks alone
+    red.append(0.02 * (rank + 1))
+    rep = sharding.distributed_report(dist, red, accum)
+    if rank == 0:
+        (Path(out_dir) / "report.json").write_text(json.dumps({"rep": rep, "sum": accum[0, 0, 0].item()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distributed_report_fields(tmp_path):
+    """the bench JSON of an N > 1 run records the backend the process
+    group ran (\"nccl\" = RCCL on the GPU node, gloo here), the rank count it saw and the mean reduce
+    time per step, max over ranks; the step's reduce sums the ranks' accumulators on rank 0."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    from optixpathtracer_amd import sharding
+
+    world = 2
+    mp.spawn(_report_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    d = json.loads((tmp_path / "report.json").read_text())
+    rep = d["rep"]
+    assert rep["backend"] == "gloo"
+    assert rep["world_size"] == world
+    assert rep["steps"] == 4
+    assert rep["reduce_ms_per_step"] >= 1e3 * 0.04 / 4  # rank 1's appended 40 ms, max over ranks
+    assert rep["reduce_bytes"] == 8 * 12 * 3 * 4
+    assert d["sum"] == 1.0 + 3 * 2.0  # three reduces onto rank 0 (1), each adding rank 1's 2
+    one = sharding.distributed_report(None, [0.1])
+    assert one["backend"] is None and one["world_size"] == 1

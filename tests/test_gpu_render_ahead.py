@@ -121,3 +121,76 @@ def test_render_ahead_display_path():
         a.set_render_ahead(0)
     for r in (a, b):
         r.close()
+
+
+def test_render_ahead_stats_exact():
+    """pt_get_stats counts the frames rendered ahead and the calls served from the
+    ring separately, and exactly.  Every call of `a` is served from the ring; `b` renders its own."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("layered")
+    a, b = _pair(sc, 1)
+    calls = 37  # the ramp 1 + 2 + 4 + 8 + 16 (+ 32 rendered ahead, 6 of them served)
+    _same_calls(a, b, calls)
+    sa, sb = a.stats(), b.stats()
+    assert sa["frames_served_ahead"] == calls
+    assert sa["frames_rendered_ahead"] >= calls
+    assert sa["samples"] == sa["frames_rendered_ahead"] * W * H  # no call rendered outside the ring
+    assert sb["frames_served_ahead"] == 0 and sb["frames_rendered_ahead"] == 0
+    assert sb["samples"] == calls * W * H
+    for r in (a, b):
+        r.close()
+
+
+def test_render_ahead_time_budget():
+    """A batch's estimated duration stays within pt_set_render_ahead_budget: with a budget below one
+    frame's time every call renders exactly its own frame into the ring (no frame is rendered that
+    no call asked for), and the images stay bit-identical."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("layered")
+    a, b = _pair(sc, 1)
+    a.set_render_ahead_budget(1e-6)
+    _same_calls(a, b, 2)  # the first batch is measured before the budget can apply
+    a.stats_reset()
+    _same_calls(a, b, 20)
+    sa = a.stats()
+    assert sa["frames_served_ahead"] == 20
+    assert sa["frames_rendered_ahead"] == 20
+    a.set_render_ahead_budget(0)  # no bound: the ramp runs again
+    _same_calls(a, b, 40)
+    assert a.stats()["frames_rendered_ahead"] > 60
+    with pytest.raises(Exception):
+        a.set_render_ahead_budget(-1.0)
+    for r in (a, b):
+        r.close()
+
+
+def test_render_ahead_debug_pixel():
+    """with a debug pixel set every call renders its own frame (no ring), so the
+    debug records belong to the call that rendered the debug frame, also after pt_set_debug_pixel
+    is called again with the same arguments."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.tiny_scene("layered")
+    a, b = _pair(sc, 0)
+    _same_calls(a, b, 12)  # the ring holds frames ahead of the debug frame
+    target = a.frame_id + 3
+    for r in (a, b):
+        r.set_debug_pixel(W // 2, H // 2, target)
+    served = a.stats()["frames_served_ahead"]
+    _same_calls(a, b, 5)
+    assert a.stats()["frames_served_ahead"] == served
+    ra, rb = a.debug_path(), b.debug_path()
+    assert len(ra) > 0 and ra == rb
+    for r in (a, b):  # the same arguments again: records cleared and rewritten by the next call
+        r.frame_id = target - 1
+        r.set_debug_pixel(W // 2, H // 2, target)
+    _same_calls(a, b, 1)
+    assert a.debug_path() == rb
+    for r in (a, b):
+        r.set_debug_pixel(-1, -1, 0)
+    _same_calls(a, b, 10)
+    assert a.stats()["frames_served_ahead"] > served
+    for r in (a, b):
+        r.close()

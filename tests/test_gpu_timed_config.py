@@ -7,10 +7,13 @@ timing on.  Here the same renderer state renders 130 frames -- batches of 64, 64
 so both streams run and the last batch is partial -- and bands of rows must equal the oracle's
 sum over the same frame ids bit for bit (the kernels and the oracle share the path's
 arithmetic).  Scenes: configs[1] (Lambert), configs[2] (Default: conductor
-spheres + layered walls) and configs[3] (i) (Dielectric, lights x20).
+spheres + layered walls), configs[3] (i) (Dielectric, lights x20), configs[3] (ii) (Layered) and
+configs[4] (the 249,740-triangle Sponza-class atrium, Default mode: the bucketed NEE / sample
+queues over the big BVH).
 
-Reference: SamplePath devicePrograms.cu:625-664 (the path loop) and OptixView.cpp:232-245
-(accumulation in frame order).
+Reference: SamplePath devicePrograms.cu:625-664 (the path loop), GlossyDiffuse.h:141-524 (the
+layered BSDF of the Default / Layered modes) and OptixView.cpp:232-245 (accumulation in frame
+order).
 """
 import numpy as np
 import pytest
@@ -26,7 +29,8 @@ FIRST = 1
 BANDS = [(532, 540), (200, 206)]
 
 
-@pytest.mark.parametrize("scene_name", ["sphere_box_diffuse", "sphere_box_conductor", "sphere_box_dielectric20"])
+@pytest.mark.parametrize("scene_name", ["sphere_box_diffuse", "sphere_box_conductor", "sphere_box_dielectric20",
+                                        "sphere_box_layered", "sponza_class"])
 def test_timed_configuration_bands_bit_exact(scene_name):
     from optixpathtracer_amd import scenes
 

@@ -2,6 +2,11 @@
 """Quick performance probe: kernel time, Msamples/s and traversal statistics per config.
 
     python tools/perf_probe.py [--scene sphere_box_diffuse] [--spp 16] [--modes 1] [--stats]
+
+Every run prints the device identity first, and every result line carries the per-kernel split
+of the render (pt_set_kernel_timing: trace kernels and the dominant shading kernel, summed HIP
+event time per launch), so an outlier run can be attributed to a kernel without a rerun
+(VERDICT round 3 item 6).
 """
 from __future__ import annotations
 
@@ -30,6 +35,16 @@ def main():
     ap.add_argument("--builders", default="0", help="0 = PLOC, 1 = LBVH")
     ap.add_argument("--streams", default="", help="wavefront streams to sweep (pt_set_wavefront_streams)")
     a = ap.parse_args()
+    import os
+    import socket
+
+    import torch  # before libptamd holds the device (torch's own HIP runtime must see it first)
+
+    p = torch.cuda.get_device_properties(0)
+    print(json.dumps({"device": p.name, "gcn_arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
+                      "host": socket.gethostname(), "pid": os.getpid(),
+                      "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")}),
+          flush=True)
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import setup_renderer
 
@@ -38,6 +53,7 @@ def main():
     for builder in [int(b) for b in a.builders.split(",")]:
         t0 = time.time()
         r = setup_renderer(sc, a.width, a.height, a.depth, bvh_builder=builder)
+        r.set_kernel_timing(True)
         st = r.stats()
         print(json.dumps({"scene": a.scene, "tris": sc.n_triangles, "builder": builder,
                           "setup_s": round(time.time() - t0, 2),
@@ -55,6 +71,7 @@ def main():
                     r.render_frames(1, min(a.spp, fpl))  # warm (also sizes the wavefront queues)
                     r.synchronize()
                     best = None
+                    runs = []
                     for rep in range(a.repeat):
                         r.stats_reset()
                         t0 = time.perf_counter()
@@ -62,12 +79,20 @@ def main():
                         r.synchronize()
                         ms = (time.perf_counter() - t0) * 1e3  # wall clock, as bench.py
                         s = r.stats()
+                        tl, sl = max(1, s["trace_kernel_launches"]), max(1, s["shade_kernel_launches"])
+                        # per-kernel split of this run: summed event windows per launch (with two
+                        # streams a window includes the time it shares the GPU with the other stream)
+                        runs.append({"wall_ms": round(ms, 2), "trace_ms": round(s["trace_kernel_ms"], 2),
+                                     "trace_ms_per_launch": round(s["trace_kernel_ms"] / tl, 4),
+                                     "shade_ms": round(s["shade_kernel_ms"], 2),
+                                     "shade_ms_per_launch": round(s["shade_kernel_ms"] / sl, 4)})
                         best = ms if best is None else min(best, ms)
                     samples = a.width * a.height * a.spp
                     out = {"kernel": kernel, "mode": mode, "fpl": fpl, **({"streams": nstr} if nstr else {}),
                            "wall_ms": round(best, 2),
                            "msamples_s": round(samples / best / 1e3, 2),
-                           "segments_per_sample": round(s["segments"] / samples, 4)}
+                           "segments_per_sample": round(s["segments"] / samples, 4),
+                           "runs": runs}
                     if a.stats:
                         r.set_traversal_stats(True)
                         r.stats_reset()

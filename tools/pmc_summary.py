@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--waves", type=int, default=6)
     ap.add_argument("--source", default="")
     ap.add_argument("--vmem-json", default=None)
+    ap.add_argument("--shade-json", default=None,
+                    help="write the VALU figures of a shading kernel (k_shade_nee) that bench.py reports as "
+                         "roofline.valu (profiles/shade_valu_config<C>.json)")
     ap.add_argument("--cus", type=int, default=256)
     ap.add_argument("--xcds", type=int, default=8)
     a = ap.parse_args()
@@ -73,6 +76,19 @@ def main():
             "valu_busy": round(min(1.0, issue * a.waves / 2.0), 3),
             "lane_utilisation": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 3),
             "wait_per_wave_cycle": round(g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES"), 3) if g("SQ_WAIT_ANY") else None,
+        }, indent=1) + "\n")
+    if a.shade_json and g("SQ_INSTS_VALU") and g("SQ_ACTIVE_INST_VALU") and g("SQ_THREAD_CYCLES_VALU"):
+        Path(a.shade_json).write_text(json.dumps({
+            "kernel": kname,
+            "source": a.source or f"tools/pmc.sh -> {root}",
+            "sources_sha": kernel_sources_sha(),
+            "dispatches": len(acc["SQ_INSTS_VALU"]),
+            "valu_insts_per_dispatch": round(g("SQ_INSTS_VALU")),
+            "lane_utilisation": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 3),
+            "valu_issue_per_wave_cycle": round(g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES"), 3)
+            if g("SQ_WAVE_CYCLES") else None,
+            "wait_per_wave_cycle": round(g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES"), 3)
+            if g("SQ_WAIT_ANY") and g("SQ_WAVE_CYCLES") else None,
         }, indent=1) + "\n")
     if g("GRBM_GUI_ACTIVE") and g("TA_TA_BUSY_sum") and g("TD_TD_BUSY_sum"):
         cyc = g("GRBM_GUI_ACTIVE") / a.xcds  # per-XCD active cycles of the dispatch
