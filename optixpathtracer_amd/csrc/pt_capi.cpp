@@ -111,7 +111,6 @@ struct pt_renderer {
     hipStream_t wf_stream(int k) const { return k ? xstream[k] : stream; }
     // scene
     BNode4* d_nodes = nullptr;
-    float4* d_nodes_cm = nullptr;  // child-major copy of d_nodes (group traversal, pt_trace_group.h)
     float4* d_isect = nullptr;
     float4* d_shade = nullptr;
     int bvh_nodes = 0, bvh_depth = 0;
@@ -237,8 +236,6 @@ struct pt_renderer {
         S.n_nodes = bvh_nodes;
         S.lds_nodes = nullptr;
         S.n_lds = 0;
-        S.nodes_cm = d_nodes_cm;
-        S.lds_cm = nullptr;
         return S;
     }
     float* accum() const { return user_accum ? user_accum : d_accum; }
@@ -885,10 +882,6 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         r->bvh_ms = ms;
         r->bvh_nodes = bo.n_nodes;
         r->bvh_depth = bo.depth;
-        if (trace_group_lanes() > 1) {  // the group traversal reads the nodes child-major
-            PT_HIPC(hipMalloc(&r->d_nodes_cm, sizeof(BNode4) * std::max(1, bo.n_nodes)), "hipMalloc nodes_cm");
-            PT_HIPC(nodes_child_major(r->d_nodes, r->d_nodes_cm, bo.n_nodes, r->stream), "nodes_child_major");
-        }
         // a traversal holds at most 3 stack entries per BVH4 level; the smallest traversal stack
         // (kMinTraversalStack) must hold them, or rays could lose subtrees
         if (3 * bo.depth > kMinTraversalStack)
@@ -942,7 +935,6 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_accum64) (void)hipFree(r->d_accum64);
     (void)hipSetDevice(r->device);
     if (r->d_nodes) (void)hipFree(r->d_nodes);
-    if (r->d_nodes_cm) (void)hipFree(r->d_nodes_cm);
     if (r->d_isect) (void)hipFree(r->d_isect);
     if (r->d_shade) (void)hipFree(r->d_shade);
     if (r->d_mats) (void)hipFree(r->d_mats);

@@ -43,11 +43,6 @@ struct DevScene {
     // n_lds = 0 everywhere else
     const BNode4* lds_nodes;
     int n_lds;
-    // The same nodes child-major (8 float4 per node: child k = {lo.xyz | link}, {hi.xyz | 0} at
-    // float4 2k, 2k+1), for the group traversal in which lane k of a ray's lane group tests child
-    // k (pt_trace_group.h); lds_cm: its staged top levels (n_lds of them)
-    const float4* nodes_cm;
-    const float4* lds_cm;
 };
 
 // Material record (3 x float4 per mesh):

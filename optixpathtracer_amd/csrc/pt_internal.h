@@ -77,11 +77,6 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
                                   hipEvent_t accum_done = nullptr, const hipEvent_t* shade_events = nullptr,
                                   int* n_shade_timed = nullptr);
 
-// Lanes per ray of the wavefront trace kernels (PT_TRACE_GROUP: 1 = one ray per lane,
-// trace_range; 4 = lane groups, pt_trace_group.h), and the child-major node copy they read.
-int trace_group_lanes();
-hipError_t nodes_child_major(const BNode4* nodes, float4* out, int n_nodes, hipStream_t stream);
-
 // Render launches.
 hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,
                          hipStream_t stream);

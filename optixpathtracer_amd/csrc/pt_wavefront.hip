@@ -33,7 +33,6 @@
 #include <unordered_map>
 
 #include "pt_internal.h"
-#include "pt_trace_group.h"
 
 namespace pt {
 
@@ -415,94 +414,17 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
     }
 }
 
-// The lane-refilling loop of trace_range for lane groups (pt_trace_group.h): a wave holds 16
-// rays, one per group of four lanes, and every per-ray decision (refill, park, node or triangle
-// step) is taken by the whole group alike.  The group's first lane writes the results
-// (`finish` / `commit` run there only); every lane of a group fetches the same ray.
-template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
-__device__ __forceinline__ void trace_range_grp(const DevScene& S, int next, int end, int* stk, int stride,
-                                                TravStats& ts, Fetch fetch, Finish finish, Commit commit = Commit{}) {
-    using Tok = decltype(finish(0, *static_cast<const TravState*>(nullptr)));
-    constexpr bool kSplit = !std::is_void_v<Tok>;
-    using TokS = std::conditional_t<kSplit, Tok, int>;
-    static_assert(kTraceGroup == 4, "group loop: four lanes per ray");
-    constexpr unsigned long long kLead = 0x1111111111111111ull;  // the first lane of every group
-    const int gc = (int)(threadIdx.x & (kTraceGroup - 1));
-    TravState st;
-    int ri = -1;
-    bool done = false;
-    next = __builtin_amdgcn_readfirstlane(next);
-    end = __builtin_amdgcn_readfirstlane(end);
-    while (true) {
-        if ((int)__popcll(__ballot(ri < 0 || done) & kLead) >= PT_GRP_REFILL || next >= end) {
-            if (STATS) ts.refills++;
-            TokS tok{};
-            const bool fin = done;
-            if (done) {
-                if (gc == 0) {
-                    if constexpr (kSplit)
-                        tok = finish(ri, st);
-                    else
-                        finish(ri, st);
-                }
-                ri = -1;
-                done = false;
-            }
-            const unsigned long long m = __ballot(ri < 0) & kLead;
-            // idle groups before this one (a later lane of an idle group counts its own first lane)
-            const int pre = lane_prefix(m) - ((gc != 0 && ri < 0) ? 1 : 0);
-            if (ri < 0 && next + pre < end) {
-                ri = next + pre;
-                fetch(ri, st);
-                if (STATS && gc == 0) ts.rays++;
-                done = S.ntri <= 0;  // empty scene: no BVH root, every ray misses
-            }
-            next = min(next + (int)__popcll(m), end);
-            if constexpr (kSplit) {
-                if (fin && gc == 0) commit(tok);
-            }
-        }
-        const bool active = ri >= 0 && !done;
-        const unsigned long long act = __ballot(active) & kLead;
-        if (!act && !__ballot(ri >= 0)) break;  // single back edge, as in trace_range
-        const int n_act = __popcll(act);
-        const int n_leaf = __popcll(__ballot(active && st.leaf != kEmptyChild) & kLead);
-        const int n_node = __popcll(__ballot(active && st.cur >= 0) & kLead);
-        const bool tri_ok = n_leaf >= min(PT_GRP_TRI, n_act) || 2 * n_node < n_act;
-        if (STATS) {
-            ts.steps++;
-            ts.active += n_act;
-            ts.node_steps += n_node > 0;
-            ts.tri_steps += tri_ok && n_leaf > 0;
-        }
-        if (tri_ok && active && st.leaf != kEmptyChild) {
-            grp_tri_step<ANY, STATS, TEX>(S, st, gc, ts);
-            if (is_any<ANY>(st) && st.h.tri >= 0) done = true;
-        }
-        if (active && !done && grp_node_step<STATS>(S, st, stk, stride, gc, ts)) done = true;
-    }
-}
-
-// A trace kernel's queue range [first, end) through the configured traversal: the workgroup's
-// LDS (stack, staged top BVH levels, triangle batches) and the loop of PT_TRACE_GROUP.
+// A trace kernel's queue range [first, end): the workgroup's LDS (per-lane stacks, the staged top
+// BVH levels, the triangle batches), then the lane-refilling loop.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_queue(DevScene S, int first, int end, TravStats& ts, Fetch fetch, Finish finish,
                                             Commit commit = Commit{}) {
-    if constexpr (kTraceGroup > 1) {
-        constexpr int kRays = kBlockWF / kTraceGroup;
-        __shared__ int gstack[kGrpStack * kRays];  // [entry][ray]: a wave's 16 rays on 16 banks
-        __shared__ float4 gtop[(kLdsNodes > 0 ? kLdsNodes : 1) * 8];
-        stage_top_cm<kLdsNodes>(S, gtop);
-        trace_range_grp<ANY, STATS, TEX>(S, first, end, gstack + threadIdx.x / kTraceGroup, kRays, ts, fetch, finish,
-                                         commit);
-    } else {
-        __shared__ int stack[kStack * kBlockWF];
-        __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
-        __shared__ TriBatchLds tri_batch[kTriBatchWaves];
-        stage_top_nodes<kLdsNodes>(S, top);
-        trace_range<ANY, STATS, TEX>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, fetch,
-                                     finish, commit);
-    }
+    __shared__ int stack[kStack * kBlockWF];
+    __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
+    __shared__ TriBatchLds tri_batch[kTriBatchWaves];
+    stage_top_nodes<kLdsNodes>(S, top);
+    trace_range<ANY, STATS, TEX>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, fetch, finish,
+                                 commit);
 }
 
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
@@ -1131,20 +1053,6 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_smp(DevScene 
     }
 }
 
-// Child-major node copy for the group traversal: child k of node n at float4 8n + 2k, 2k + 1 as
-// {lo.xyz | link}, {hi.xyz | 0}.  One thread per (node, child).
-__global__ __launch_bounds__(kBlockWF) void k_nodes_cm(const BNode4* __restrict__ in, float4* __restrict__ out,
-                                                       int n_nodes) {
-    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= 4 * n_nodes) return;
-    const int n = i >> 2, k = i & 3;
-    const BNode4& a = in[n];
-    auto comp = [k](const float4 v) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
-    const int link = k == 0 ? a.child.x : k == 1 ? a.child.y : k == 2 ? a.child.z : a.child.w;
-    out[8 * n + 2 * k] = make_float4(comp(a.lox), comp(a.loy), comp(a.loz), __int_as_float(link));
-    out[8 * n + 2 * k + 1] = make_float4(comp(a.hix), comp(a.hiy), comp(a.hiz), 0.0f);
-}
-
 __global__ __launch_bounds__(kBlockWF) void k_accum(WFState W, DevLaunch L, int nf) {
     const int P = L.width * L.height;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
@@ -1292,14 +1200,6 @@ hipError_t launch_shade_mode(int mode, bool fused, const DevScene& S, const DevL
 hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStream_t stream) {
     const unsigned blocks = (unsigned)std::min<size_t>((n + kBlockWF - 1) / kBlockWF, 8192);
     hipLaunchKernelGGL(k_f64_to_f32, dim3(std::max(1u, blocks)), dim3(kBlockWF), 0, stream, sum64, sum32, n);
-    return hipGetLastError();
-}
-
-int trace_group_lanes() { return kTraceGroup; }
-
-hipError_t nodes_child_major(const BNode4* nodes, float4* out, int n_nodes, hipStream_t stream) {
-    if (n_nodes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_nodes_cm, item_grid(4 * n_nodes, kBlockWF), dim3(kBlockWF), 0, stream, nodes, out, n_nodes);
     return hipGetLastError();
 }
 
