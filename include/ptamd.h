@@ -193,6 +193,11 @@ int pt_set_primary_dedup(pt_renderer* r, int32_t enable);
  * one batch's kernels overlap another's; the batches still add into the sum in frame order, and
  * the image is bit-identical to 1.  A call uses at most as many streams as it has batches. */
 int pt_set_wavefront_streams(pt_renderer* r, int32_t streams);
+/* Wavefront, a call of one frame (pt_render without render-ahead, pt_render_frames with n = 1,
+ * pt_launch): with 2 or more wavefront streams, the frame's rows are split into two bands that
+ * render on two streams at once, each band's kernels filling the other's SIMT tails (default 1).
+ * Every pixel's path depends only on its pixel and frame id: the image is bit-identical to 0. */
+int pt_set_band_split(pt_renderer* r, int32_t enable);
 
 /* LaunchParams (Renderer/OptiX/LaunchParams.h:9-28) as a C struct: the state one optixLaunch
  * reads.  Same fields and meaning; device pointers where the reference holds device pointers

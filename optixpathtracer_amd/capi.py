@@ -177,6 +177,7 @@ SIGNATURES = {
     "pt_accum_clear": (C.c_int, [_R]),
     "pt_render_frames": (C.c_int, [_R, C.c_uint32, C.c_uint32]),
     "pt_set_primary_dedup": (C.c_int, [_R, C.c_int32]),
+    "pt_set_band_split": (C.c_int, [_R, C.c_int32]),
     "pt_set_wavefront_streams": (C.c_int, [_R, C.c_int32]),
     "pt_render_accumulate": (C.c_int, [_R, C.c_uint32, C.c_uint32, _FP]),
     "pt_set_accum_device_buffer": (C.c_int, [_R, C.c_void_p]),

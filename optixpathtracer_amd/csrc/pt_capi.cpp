@@ -191,6 +191,7 @@ struct pt_renderer {
     // optional per-launch timing of the wavefront's closest-hit trace kernel (k_extend)
     bool kernel_timing = false;
     bool primary_dedup = true;  // pt_set_primary_dedup
+    bool band_split = true;     // pt_set_band_split: one-frame calls render two row bands on two streams
     EventPool tev;
     std::vector<hipEvent_t> tev_frame;  // 2 * (max_bounces + 1) events handed to one frame
     double trace_ms = 0.0;
@@ -272,6 +273,8 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
     DevLaunch L;
     L.width = r->width;
     L.height = r->height;
+    L.row0 = 0;
+    L.image_height = r->height;
     std::memcpy(L.cam_pos, r->cam_pos, sizeof L.cam_pos);
     std::memcpy(L.inv_view, r->inv_view, sizeof L.inv_view);
     std::memcpy(L.inv_proj, r->inv_proj, sizeof L.inv_proj);
@@ -327,7 +330,12 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // VALU-bound tracing of the other, and each kernel's SIMT tail filled); k_accum still adds
         // the batches in frame order (accum_wait / accum_done)
         const int nbatch = (int)((n + (uint32_t)nf_cap - 1) / (uint32_t)nf_cap);
-        int ns = std::max(1, std::min(r->wf_streams, nbatch));
+        // One frame (pt_render / pt_display_add_frame without render-ahead, the path a viewer that
+        // moves the camera every frame gets): its rows split into two bands, one per stream, so
+        // each band's kernels fill the other's SIMT tails.  Every pixel's path depends only on its
+        // pixel and frame id, so the image is the same bit for bit.
+        const bool bands = n == 1 && r->band_split && r->height > 1;
+        int ns = std::max(1, std::min(r->wf_streams, bands ? 2 : nbatch));
         for (int k = 0; k < ns; ++k) {
             WFState& w = k ? r->xwf[k] : r->wf;
             if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces) {
@@ -364,11 +372,20 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             PT_HIP(hipEventRecord(r->ev_fork, r->stream), "hipEventRecord");
             for (int k = 1; k < ns; ++k) PT_HIP(hipStreamWaitEvent(r->xstream[k], r->ev_fork, 0), "hipStreamWaitEvent");
         }
+        const int nband = bands && ns > 1 ? 2 : 1;  // row bands of a one-frame call
         int batch = 0;
         for (uint32_t f = 0; f < n; ++batch) {  // one event pair per batch (the batch's kernel chain)
             const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
             DevLaunch L = make_launch(r, frame_stride ? accum + (size_t)f * frame_stride : accum, first + f,
                                       (uint32_t)nf, accum64, frame_stride);
+            const int band = nband > 1 ? batch : 0;
+            if (nband > 1) {  // rows [row0, row0 + height) of the frame; the sum buffers at the band
+                L.row0 = band == 0 ? 0 : r->height / 2;
+                L.height = band == 0 ? r->height / 2 : r->height - r->height / 2;
+                const size_t off = 3 * (size_t)r->width * (size_t)L.row0;
+                L.accum += off;
+                if (L.accum64) L.accum64 += off;
+            }
             const int sk = batch % ns;  // stream of this batch
             hipStream_t st = r->wf_stream(sk);
             if (!dual) {
@@ -391,13 +408,14 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             int n_timed = 0, n_stimed = 0;
             PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, sk ? r->xwf[sk] : r->wf, first + f,
                                           nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
-                                          dual && batch > 0 ? r->ev_accum[(batch - 1) & 1] : nullptr,
-                                          dual ? r->ev_accum[batch & 1] : nullptr, sev, &n_stimed),
+                                          // batches add into the sum in frame order; bands touch disjoint pixels
+                                          dual && batch > 0 && nband == 1 ? r->ev_accum[(batch - 1) & 1] : nullptr,
+                                          dual && nband == 1 ? r->ev_accum[batch & 1] : nullptr, sev, &n_stimed),
                    "wavefront launch");
             if (tev) r->tev.give_back((size_t)(r->max_bounces + 1 - n_timed));  // pairs never recorded
             if (sev) r->sev.give_back((size_t)(r->max_bounces + 1 - n_stimed));
             if (!dual) PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
-            f += (uint32_t)nf;
+            if (band + 1 == nband) f += (uint32_t)nf;
         }
         if (dual) {
             for (int k = 1; k < ns; ++k) {
@@ -1604,6 +1622,17 @@ extern "C" int pt_set_primary_dedup(pt_renderer* r, int32_t enable) {
     r->primary_dedup = enable != 0;
     for (pt_renderer* p : r->peers) {
         if ((rc = pt_set_primary_dedup(p, enable)) != PT_OK) return rc;
+    }
+    return PT_OK;
+}
+
+extern "C" int pt_set_band_split(pt_renderer* r, int32_t enable) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_band_split: NULL");
+    int rc = collect_pending(r);
+    if (rc) return rc;
+    r->band_split = enable != 0;
+    for (pt_renderer* p : r->peers) {
+        if ((rc = pt_set_band_split(p, enable)) != PT_OK) return rc;
     }
     return PT_OK;
 }

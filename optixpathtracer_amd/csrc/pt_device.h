@@ -55,7 +55,12 @@ struct DevLight {
 };
 
 struct DevLaunch {
-    int width, height;
+    int width, height;  // height: the rows of this launch (a band of the image, see row0)
+    // A launch may render a band of rows [row0, row0 + height) of an image image_height rows high
+    // (the one-frame path splits a frame into two bands on the two wavefront streams): the camera
+    // ray, the path seed and the debug pixel use the image's row and pixel index, everything else
+    // the band's own pixel index p (image pixel = p + width * row0), and accum points at the band.
+    int row0, image_height;
     float cam_pos[3];
     float inv_view[16];
     float inv_proj[16];
@@ -81,10 +86,12 @@ struct DevLaunch {
 constexpr int kDebugMaxBounces = 64;
 constexpr int kDebugRecordFloats = 22;  // ptamd.h pt_debug_bounce
 
-// Wavefront path id of the debug path in the batch of L (path = frame offset * pixels + pixel), or -1.
+// Wavefront path id of the debug path in the batch of L (path = frame offset * pixels + pixel, in
+// the launch's band), or -1.
 __device__ __forceinline__ int debug_path_id(const DevLaunch& L) {
     const uint32_t f = L.debug_frame - L.frame_base;
-    return (L.debug_pixel >= 0 && f < L.n_frames) ? (int)f * L.width * L.height + L.debug_pixel : -1;
+    const int P = L.width * L.height, p = L.debug_pixel - L.width * L.row0;  // the band's pixel index
+    return (L.debug_pixel >= 0 && p >= 0 && p < P && f < L.n_frames) ? (int)f * P + p : -1;
 }
 
 struct Hit {
@@ -768,10 +775,10 @@ __device__ __forceinline__ bool traverse(const DevScene& S, f3 o, f3 d, float tm
     return s.h.tri >= 0;
 }
 
-// devicePrograms.cu:601-623 — pixel-centre primary ray.
+// devicePrograms.cu:601-623 — pixel-centre primary ray (y: the launch's row, row0 + y the image's).
 __device__ __forceinline__ void camera_ray(const DevLaunch& L, int x, int y, f3& o, f3& d) {
     float xs = ((float)x + 0.5f) / (float)L.width;
-    float ys = ((float)y + 0.5f) / (float)L.height;
+    float ys = ((float)(y + L.row0) + 0.5f) / (float)L.image_height;
     float ndc[4] = {xs * 2.0f - 1.0f, ys * 2.0f - 1.0f, 1.0f, 1.0f};
     float pv[4], pw[4];
     mat4_mul_vec4(L.inv_proj, ndc, pv);

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uin
         camera_ray(L, x, y, o, d);
         W.ray_o[0][q] = make_float4(o.x, o.y, o.z, __int_as_float(q));
         W.ray_d[0][q] = make_float4(d.x, d.y, d.z, 0.0f);
-        const uint32_t seed = tea16((uint32_t)(L.width * y + x), frame0 + (uint32_t)f);  // devicePrograms.cu:631
+        const uint32_t seed = tea16((uint32_t)(L.width * (y + L.row0) + x), frame0 + (uint32_t)f);  // devicePrograms.cu:631
         W.beta[q] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(seed));
         W.L[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
                 SurfaceHit sf;
                 reconstruct<TEX>(S, h, d, sf);
                 if (shade0) {
-                    seed = tea16((uint32_t)(path % P1), L.frame_base + (uint32_t)(path / P1));
+                    seed = tea16((uint32_t)(path % P1 + L.width * L.row0), L.frame_base + (uint32_t)(path / P1));
                     beta = mk(1.0f, 1.0f, 1.0f);
                 } else {
                     float4 bv = kBetaQ ? bv_q : ldqs(W.beta + path);
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
         uint32_t seed = 0;
         float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (valid && tri >= 0) {
-            seed = tea16((uint32_t)p, L.frame_base + (uint32_t)f);  // devicePrograms.cu:631
+            seed = tea16((uint32_t)(p + L.width * L.row0), L.frame_base + (uint32_t)f);  // devicePrograms.cu:631
             if (path == dbg) debug_record(L, 1, __float_as_int(S.isect[3 * tri].w), sf, beta, mk(0.0f, 0.0f, 0.0f));
             const bool conductor = rnd(seed) < sf.metallic;  // :400
             int li;

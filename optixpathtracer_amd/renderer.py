@@ -214,6 +214,10 @@ class OptixRenderer:
     def set_wavefront_streams(self, streams: int) -> None:
         check(self.lib.pt_set_wavefront_streams(self.h, int(streams)), "pt_set_wavefront_streams")
 
+    def set_band_split(self, enable: bool) -> None:
+        """One-frame calls: two row bands on two wavefront streams (pt_set_band_split, default on)."""
+        check(self.lib.pt_set_band_split(self.h, 1 if enable else 0), "pt_set_band_split")
+
     def render_accumulate(self, spp: int, first_frame_id: int = 1) -> np.ndarray:
         """Clear, render frame ids first_frame_id .. +spp-1 and return the mean image
         (pt_render_accumulate); the sum stays in the device accumulator."""

@@ -36,6 +36,18 @@ def main():
     for _ in range(8):
         r.Render(buf)
     out = {"scene": a.scene, "calls": a.calls}
+    for band in (True, False):  # pt_set_band_split: the frame as two row bands on two streams
+        r.set_band_split(band)
+        best = None
+        for _ in range(a.repeat):
+            t = time.perf_counter()
+            for _ in range(a.calls):
+                r.Render(buf)
+            r.synchronize()
+            ms = (time.perf_counter() - t) / a.calls * 1e3
+            best = ms if best is None else min(best, ms)
+        out[f"ms_per_call_{'bands' if band else 'one_band'}"] = round(best, 3)
+    r.set_band_split(True)
     for kind in ("fresh", "reuse"):
         best = None
         for _ in range(a.repeat):

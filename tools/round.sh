@@ -30,4 +30,16 @@ else
   echo "[round] pmc (TA / TD / TCP passes, Lambert, 64 frames)"
   timeout -k 10 600 tools/pmc_ta.sh gpurun_out/pmcta_$TAG --fpl 64 --spp 64 > "$OUT/pmc_ta.log" 2>&1
   tail -1 "$OUT/pmc_ta.log"
+  # VALU issue of k_shade_nee, the dominant kernel of the Default / Layered configs (bench.py
+  # roofline.valu reads profiles/shade_valu_config<C>.json): one SQ pass per config
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  for c in 3:sphere_box_conductor 4l:sphere_box_layered 5:sponza_class; do
+    cfg=${c%%:*}; sc=${c#*:}
+    echo "[round] shade VALU pass, config $cfg"
+    timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU \
+      --output-format csv -d "$OUT/shv_$cfg" -o run -- python3 tools/perf_probe.py --scene $sc --fpl 64 --spp 64 --repeat 1 \
+      > "$OUT/shv_$cfg.log" 2>&1
+    python3 tools/pmc_summary.py "$OUT/shv_$cfg" k_shade_nee --shade-json "$OUT/shade_valu_config$cfg.json" \
+      --source "tools/round.sh $TAG profile (rocprofv3 SQ pass, perf_probe --scene $sc --fpl 64 --spp 64)" | tail -3
+  done
 fi
