@@ -81,7 +81,7 @@ def test_band_split_textured_and_display():
 
 def test_band_split_launch_params():
     """pt_launch (LaunchParams + optixLaunch) renders one frame into the caller's device buffer."""
-    import torch
+    from test_gpu_parity import _HipBuffers
 
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import camera_from_blender
@@ -89,15 +89,18 @@ def test_band_split_launch_params():
     sc = scenes.tiny_scene("conductor")
     w, h, depth = 72, 41, 5
     p, iv, ip = camera_from_blender(sc.camera_blender_pos, sc.camera_blender_rot, sc.fov_deg, w, h)
-    lights = torch.from_numpy(np.ascontiguousarray(sc.lights, np.float32)).cuda()
     out = []
     for band in (True, False):
         r = _renderer(sc, w, h, depth, 0, band)
-        buf = torch.full((h, w, 3), float("nan"), dtype=torch.float32, device="cuda")
-        torch.cuda.synchronize()
-        r.launch(buf.data_ptr(), (w, h), 9, p, iv, ip, lights.data_ptr(), len(sc.lights), depth)
+        hb = _HipBuffers()
+        lights = hb.alloc(sc.lights.nbytes)
+        hb.upload(lights, sc.lights.astype(np.float32))
+        buf = hb.alloc(w * h * 3 * 4)
+        hb.upload(buf, np.full((h, w, 3), np.nan, np.float32))  # overwritten, not added
+        r.launch(buf, (w, h), 9, p, iv, ip, lights, len(sc.lights), depth)
         r.synchronize()
-        out.append(buf.cpu().numpy())
+        out.append(hb.download(buf, (h, w, 3)))
+        hb.free()
         r.close()
     assert np.isfinite(out[0]).all()
     np.testing.assert_array_equal(out[0], out[1])

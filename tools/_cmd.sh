@@ -1,14 +1,13 @@
 set -e
-O=gpurun_out/r04g
+O=gpurun_out/r04h
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-echo "[r04g] band-split GPU tests + parity subset"
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_band_split.py tests/test_gpu_render_ahead.py tests/test_gpu_bitexact.py \
-  tests/test_gpu_debug_path.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > $O/gputest.log 2>&1 \
-  || { tail -40 $O/gputest.log; exit 1; }
+echo "[r04h] parity of the hemisphere-split NEE buckets"
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_bitexact.py tests/test_gpu_parity.py tests/test_gpu_timed_config.py \
+  tests/test_gpu_debug_path.py -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || { tail -40 $O/gputest.log; exit 1; }
 tail -2 $O/gputest.log
-echo "[r04g] one-frame path"
-for s in sphere_box_diffuse sphere_box_dielectric20 sphere_box_conductor; do
-  timeout -k 10 200 python3 tools/one_frame.py --scene $s
-done > $O/one_frame.log 2>&1
-cat $O/one_frame.log | grep scene
+echo "[r04h] A/B"
+tools/ab.sh "base nsplit" 3 --scene sphere_box_conductor --fpl 64 --spp 64 > $O/ab_c3.log 2>&1
+tools/ab.sh "base nsplit" 2 --scene sphere_box_layered --fpl 64 --spp 64 > $O/ab_4l.log 2>&1
+tools/ab.sh "base nsplit" 2 --scene sponza_class --fpl 64 --spp 64 > $O/ab_5.log 2>&1
+python3 tools/ab_summary.py $O/ab_c3.log $O/ab_4l.log $O/ab_5.log
