@@ -176,6 +176,11 @@ struct pt_renderer {
     bool spec_pending = false;      // a look-ahead batch was enqueued since the last collect
     hipStream_t dl_stream = nullptr;
     hipEvent_t ev_frame = nullptr;  // after the d_frame render (no ring)
+    // a one-frame call in row bands (pt_set_band_split): band 0 holds the first band0_rows rows
+    // (0: the last one-frame call was not banded); ev_band0 follows its k_accum, so pt_render can
+    // download them while band 1 still renders
+    int band0_rows = 0;
+    hipEvent_t ev_band0 = nullptr;
     uint32_t lights_version = 0;
     uint32_t debug_version = 0;  // bumped by pt_set_debug_pixel (the records are rewritten)
     float* d_display = nullptr;  // progressive view buffer (pt_display_*)
@@ -373,6 +378,11 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             for (int k = 1; k < ns; ++k) PT_HIP(hipStreamWaitEvent(r->xstream[k], r->ev_fork, 0), "hipStreamWaitEvent");
         }
         const int nband = bands && ns > 1 ? 2 : 1;  // row bands of a one-frame call
+        // band 0 is the smaller one (7/16 of the rows), so it finishes first and pt_render's
+        // download of its rows overlaps the rest of band 1
+        const int rows0 = r->height * 7 / 16;
+        r->band0_rows = nband > 1 ? rows0 : 0;
+        if (nband > 1 && !r->ev_band0) PT_HIP(hipEventCreateWithFlags(&r->ev_band0, hipEventDisableTiming), "hipEventCreate");
         int batch = 0;
         for (uint32_t f = 0; f < n; ++batch) {  // one event pair per batch (the batch's kernel chain)
             const int nf = (int)std::min<uint32_t>((uint32_t)nf_cap, n - f);
@@ -380,8 +390,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                                       (uint32_t)nf, accum64, frame_stride);
             const int band = nband > 1 ? batch : 0;
             if (nband > 1) {  // rows [row0, row0 + height) of the frame; the sum buffers at the band
-                L.row0 = band == 0 ? 0 : r->height / 2;
-                L.height = band == 0 ? r->height / 2 : r->height - r->height / 2;
+                L.row0 = band == 0 ? 0 : rows0;
+                L.height = band == 0 ? rows0 : r->height - rows0;
                 const size_t off = 3 * (size_t)r->width * (size_t)L.row0;
                 L.accum += off;
                 if (L.accum64) L.accum64 += off;
@@ -415,6 +425,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             if (tev) r->tev.give_back((size_t)(r->max_bounces + 1 - n_timed));  // pairs never recorded
             if (sev) r->sev.give_back((size_t)(r->max_bounces + 1 - n_stimed));
             if (!dual) PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
+            if (nband > 1 && band == 0) PT_HIP(hipEventRecord(r->ev_band0, st), "hipEventRecord");
             if (band + 1 == nband) f += (uint32_t)nf;
         }
         if (dual) {
@@ -564,7 +575,8 @@ int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t f
 // one-frame sum into zeros that the plain path computes, bit for bit.  The debug pixel's records
 // belong to the call that renders its frame, so with a debug pixel set every call renders its
 // own frame.
-int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nullptr, bool look_ahead = false) {
+int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nullptr, bool look_ahead = false,
+                       hipEvent_t* part_ready = nullptr, size_t* part_floats = nullptr) {
     const size_t n3 = 3 * (size_t)r->width * (size_t)r->height;
     const int kernel = r->kernel == PT_KERNEL_AUTO ? PT_KERNEL_WAVEFRONT : r->kernel;
     const uint32_t f = r->frame_id;
@@ -627,6 +639,10 @@ int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nu
     const int rc = launch_frames(r, r->d_frame, f, 1);
     if (rc) return rc;
     *img = r->d_frame;
+    if (part_ready && r->band0_rows > 0) {  // the first band's rows are final once ev_band0 passes
+        *part_ready = r->ev_band0;
+        *part_floats = 3 * (size_t)r->width * (size_t)r->band0_rows;
+    }
     if (ready) {
         if (!r->ev_frame) PT_HIP(hipEventCreateWithFlags(&r->ev_frame, hipEventDisableTiming), "hipEventCreate");
         PT_HIP(hipEventRecord(r->ev_frame, r->stream), "hipEventRecord");
@@ -972,7 +988,7 @@ int pt_destroy(pt_renderer* r) {
         if (r->xstream[k]) (void)hipStreamDestroy(r->xstream[k]);
         if (r->ev_join[k]) (void)hipEventDestroy(r->ev_join[k]);
     }
-    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1], r->ring[0].ready, r->ring[1].ready,
+    for (hipEvent_t e : {r->ev_fork, r->ev_accum[0], r->ev_accum[1], r->ev_band0, r->ring[0].ready, r->ring[1].ready,
                          r->ring[0].start, r->ring[1].start, r->ev_frame})
         if (e) (void)hipEventDestroy(e);
     if (r->dl_stream) (void)hipStreamDestroy(r->dl_stream);
@@ -1102,12 +1118,21 @@ int pt_render(pt_renderer* r, float* host_rgb) {
     r->frame_id++;  // :623
     size_t bytes = sizeof(float) * 3 * (size_t)r->width * (size_t)r->height;
     const float* img = nullptr;
-    hipEvent_t ready = nullptr;
-    int rc = render_frame_image(r, &img, &ready, true);
+    hipEvent_t ready = nullptr, part = nullptr;
+    size_t part_floats = 0;
+    int rc = render_frame_image(r, &img, &ready, true, &part, &part_floats);
     if (rc) return rc;
     // the download runs on its own stream after the image's event, so a look-ahead batch that
     // render_frame_image enqueued on r->stream keeps rendering while this frame is copied
     if (!r->dl_stream) PT_HIP(hipStreamCreateWithFlags(&r->dl_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (part) {  // a banded frame: its first band's rows while the second band renders
+        PT_HIP(hipStreamWaitEvent(r->dl_stream, part, 0), "hipStreamWaitEvent");
+        PT_HIP(hipMemcpyAsync(host_rgb, img, sizeof(float) * part_floats, hipMemcpyDeviceToHost, r->dl_stream),
+               "download frame");
+        host_rgb += part_floats;
+        img += part_floats;
+        bytes -= sizeof(float) * part_floats;
+    }
     PT_HIP(hipStreamWaitEvent(r->dl_stream, ready, 0), "hipStreamWaitEvent");
     PT_HIP(hipMemcpyAsync(host_rgb, img, bytes, hipMemcpyDeviceToHost, r->dl_stream), "download frame");
     PT_HIP(hipStreamSynchronize(r->dl_stream), "hipStreamSynchronize");

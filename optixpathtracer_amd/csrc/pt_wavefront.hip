@@ -39,6 +39,14 @@ namespace pt {
 namespace {
 
 constexpr int kBlockWF = 256;
+// Trace kernels (k_extend, k_trace_pair, k_shadow_vis): workgroup size.  Every workgroup holds its
+// own copy of the staged top BVH levels in LDS, so fewer, larger workgroups per CU leave room for
+// more staged nodes at the same waves per SIMD: 512 threads with 100 nodes / 768 with 150 lost
+// 2.9 / 7.0 % Lambert and 1.7 / 3.8 % Dielectric, Sponza-class +0.6 %.
+#ifndef PT_TRACE_BLOCK
+#define PT_TRACE_BLOCK 256
+#endif
+constexpr int kBlockTrace = PT_TRACE_BLOCK;
 // LDS traversal stack entries per lane (PT_WF_STACK, pt_device.h): 11 KB per workgroup.
 constexpr int kStack = PT_WF_STACK;
 // Top BVH4 levels staged in LDS per trace workgroup (nodes 0 .. kLdsNodes-1, breadth-first: 49 =
@@ -53,7 +61,7 @@ constexpr int kStack = PT_WF_STACK;
 #endif
 constexpr int kLdsNodes = PT_LDS_NODES;
 // wave-batched triangle tests (pt_device.h wave_tri_batch): 2.25 KB of LDS per wave
-constexpr int kTriBatchWaves = kBlockWF / 64;
+constexpr int kTriBatchWaves = kBlockTrace / 64;
 // Trace kernels: 6 waves per SIMD (80 VGPRs, 3 spilled in cold paths); the textured variants
 // keep 4.
 #ifndef PT_WF_WAVES
@@ -401,7 +409,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         const uint64_t c2 = probe_clock(st.best);
         if (STATS) ts.tri_steps += (uint32_t)(c2 - c1);
 #endif
-        if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockWF, spill, ts)) done = true;
+        if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockTrace, spill, ts)) done = true;
 #if PT_CYCLE_PROBE
         if (STATS) {  // node half: until its loads landed (active), the rest (node_steps)
             const uint64_t c4 = probe_clock(st.cur);
@@ -419,7 +427,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_queue(DevScene S, int first, int end, TravStats& ts, Fetch fetch, Finish finish,
                                             Commit commit = Commit{}) {
-    __shared__ int stack[kStack * kBlockWF];
+    __shared__ int stack[kStack * kBlockTrace];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
     __shared__ TriBatchLds tri_batch[kTriBatchWaves];
     stage_top_nodes<kLdsNodes>(S, top);
@@ -440,7 +448,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats&
 // and each hit record is written to all copies.  The records are bit-identical to tracing every
 // copy; DESIGN.md §5 gives the A/B.
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_extend(DevScene S, WFState W, int b, int dup,
+__global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_extend(DevScene S, WFState W, int b, int dup,
                                                                   int copies, unsigned long long* counters) {
     const int n = *cnt(W, b, kQueue);
     const int n_trace = n / dup;
@@ -732,7 +740,7 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
 // and one launch instead of two).  Items [0, n_ext) are extension rays (closest hit ->
 // hit records), items [n_ext, n_ext + n_sh) shadow rays (any hit -> deferred NEE add).
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockWF, wf_waves(TEX)) void k_trace_pair(DevScene S, WFState W, int b,
+__global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
     const int n_ext = *cnt(W, b + 1, kQueue);
     const int n_sh = *cnt(W, b, kShadowQ);
@@ -884,7 +892,7 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
 // table (k_shadow0_setup), vis[j] = 1 if unoccluded; table = 0: vis[j] = the ray's item code
 // if unoccluded, else -1 (k_nee_compact reads it).
 template <bool TEX>
-__global__ __launch_bounds__(kBlockWF, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b, int table,
+__global__ __launch_bounds__(kBlockTrace, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b, int table,
                                                                       unsigned long long* counters) {
     const int n = *cnt(W, b, kShadowQ);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[5], (unsigned long long)n);
@@ -1115,7 +1123,7 @@ dim3 occupancy_grid(K kernel, int cus) {
     auto it = cache.find(key);
     int per_cu = 0;
     if (it == cache.end()) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockWF, 0) != hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockTrace, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         cache[key] = per_cu;
     } else {
@@ -1283,16 +1291,16 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
         if (tex) {
             if (stats)
-                hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockWF),
+                hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockTrace),
                                    0, stream, S, W, b, dup, copies, L.counters);
             else
                 hipLaunchKernelGGL((k_extend<false, true>), occupancy_grid(k_extend<false, true>, cus),
-                                   dim3(kBlockWF), 0, stream, S, W, b, dup, copies, L.counters);
+                                   dim3(kBlockTrace), 0, stream, S, W, b, dup, copies, L.counters);
         } else if (stats) {
-            hipLaunchKernelGGL((k_extend<true, false>), occupancy_grid(k_extend<true, false>, cus), dim3(kBlockWF), 0,
+            hipLaunchKernelGGL((k_extend<true, false>), occupancy_grid(k_extend<true, false>, cus), dim3(kBlockTrace), 0,
                                stream, S, W, b, dup, copies, L.counters);
         } else {
-            hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockWF),
+            hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockTrace),
                                0, stream, S, W, b, dup, copies, L.counters);
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
@@ -1305,16 +1313,16 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         if (tex) {
             if (stats)
                 hipLaunchKernelGGL((k_trace_pair<true, true>), occupancy_grid(k_trace_pair<true, true>, cus),
-                                   dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+                                   dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
             else
                 hipLaunchKernelGGL((k_trace_pair<false, true>), occupancy_grid(k_trace_pair<false, true>, cus),
-                                   dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+                                   dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
         } else if (stats) {
             hipLaunchKernelGGL((k_trace_pair<true, false>), occupancy_grid(k_trace_pair<true, false>, cus),
-                               dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+                               dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
         } else {
             hipLaunchKernelGGL((k_trace_pair<false, false>), occupancy_grid(k_trace_pair<false, false>, cus),
-                               dim3(kBlockWF), 0, stream, S, W, b, L.counters);
+                               dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
         ++timed;
@@ -1322,10 +1330,10 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     };
     auto shadow_vis = [&](int b, int table) -> hipError_t {
         if (tex)
-            hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockWF), 0, stream,
+            hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockTrace), 0, stream,
                                S, W, b, table, L.counters);
         else
-            hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockWF), 0,
+            hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockTrace), 0,
                                stream, S, W, b, table, L.counters);
         if (!table) hipLaunchKernelGGL(k_nee_compact, item_grid(P, kBlockSh * kCompactPer), dim3(kBlockSh), 0, stream, W, b);
         return hipGetLastError();

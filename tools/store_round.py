@@ -32,6 +32,25 @@ def main():
                           str(out / f"{tag}_wavefront_kernel_stats_single_stream.csv")],
                          check=True, capture_output=True, text=True).stdout
     (out / "shade_pmc.json").write_text(pmc)
+    # SQ / TCC / TCP and TA / TD passes of k_trace_pair (roofline.valu_pmc / vmem_pmc) and the
+    # k_shade_nee VALU passes of the Default / Layered configs (roofline.valu)
+    summ = ROOT / "tools" / "pmc_summary.py"
+    if (ROOT / "gpurun_out" / f"pmc_{tag}").exists():
+        txt = subprocess.run([sys.executable, str(summ), str(ROOT / "gpurun_out" / f"pmc_{tag}"), "k_trace_pair",
+                              "--valu-json", str(out / "valu.json"), "--waves", "6",
+                              "--source", f"tools/round.sh {tag} profile (tools/pmc.sh, Lambert, 64 frames)"],
+                             check=True, capture_output=True, text=True).stdout
+        (out / f"{tag}_pmc_trace_pair_lambert.txt").write_text(txt)
+    if (ROOT / "gpurun_out" / f"pmcta_{tag}").exists():
+        txt = subprocess.run([sys.executable, str(summ), str(ROOT / "gpurun_out" / f"pmcta_{tag}"), "k_trace_pair",
+                              "--vmem-json", str(out / "vmem.json"),
+                              "--source", f"tools/round.sh {tag} profile (tools/pmc_ta.sh, Lambert, 64 frames)"],
+                             check=True, capture_output=True, text=True).stdout
+        (out / f"{tag}_pmc_ta_td_trace_pair.txt").write_text(txt)
+    for c in ("3", "4l", "5"):
+        src = rnd / f"shade_valu_config{c}.json"
+        if src.exists():
+            shutil.copyfile(src, out / f"shade_valu_config{c}.json")
 
 
 if __name__ == "__main__":
