@@ -538,6 +538,10 @@ def main():
             # timed from a state change on, ramp included, and up to the end of the last look-ahead
             # batch (frames no call asked for count as time, not as samples); the same loop with
             # render-ahead off is reported beside it.
+            # the caller's loop runs without the per-launch event pairs of the roofline fields
+            # (pt_set_kernel_timing is a diagnostic the reference's viewer does not have)
+            r.set_kernel_timing(False)
+
             def ref_loop(calls):
                 r.frame_id = 0
                 r.Render()  # the first call after a change renders its own frame only
@@ -576,9 +580,11 @@ def main():
             out["value_reference_loop"] = round(args.width * args.height * args.reference_loops / e4 / 1e6, 3)
             out["reference_loop"] = {"calls": args.reference_loops, "ms_per_call": round(e4 / args.reference_loops * 1e3, 3),
                                      "what": "pt_render: 1 spp per call, frame.id++, D2H download of the 24.9 MB "
-                                             "frame per call (the reference's DrawOptix loop), render-ahead on",
+                                             "frame per call (the reference's DrawOptix loop), render-ahead on, "
+                                             "kernel timing off",
                                      "first_call_after_change_ms": round(1e3 * statistics.median(lat), 3),
                                      "render_ahead_budget_ms": 50.0,
+                                     # one frame per call: two row bands on the two streams (pt_set_band_split)
                                      "no_render_ahead": {"calls": n_off, "ms_per_call": round(e5 / n_off * 1e3, 3),
                                                          "value": round(args.width * args.height * n_off / e5 / 1e6, 3)}}
         if world == 1 and not args.no_cpu_baseline:
