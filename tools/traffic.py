@@ -29,6 +29,12 @@ from optixpathtracer_amd.provenance import kernel_sources_sha  # noqa: E402
 GROUPS = {"k_render_mega": ("k_render_mega",), "k_extend+k_trace_pair": ("k_extend", "k_trace_pair")}
 
 
+def timed_instance(name: str) -> bool:
+    """The kernels bench.py times: not the traversal-statistics instances (template STATS = true,
+    bench.py's untimed counter render), whose counter atomics add writes of their own."""
+    return "<true" not in name
+
+
 def counter_rows(d: Path):
     for f in sorted(d.rglob("*counter_collection.csv")):
         with open(f) as fh:
@@ -41,6 +47,8 @@ def per_kernel(d: Path, counter: str):
         if row.get("Counter_Name") != counter:
             continue
         name = row["Kernel_Name"]
+        if not timed_instance(name):
+            continue
         for g, members in GROUPS.items():
             if any(k in name for k in members):
                 vals.setdefault(g, []).append(float(row["Counter_Value"]))
@@ -52,6 +60,8 @@ def kernel_stats(d: Path):
     for f in sorted(d.rglob("*kernel_stats.csv")):
         with open(f) as fh:
             for row in csv.DictReader(fh):
+                if not timed_instance(row["Name"]):
+                    continue
                 for g, members in GROUPS.items():
                     if any(k in row["Name"] for k in members):
                         o = out.setdefault(g, {"calls": 0, "total_ns": 0.0})
