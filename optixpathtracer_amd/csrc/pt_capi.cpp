@@ -313,6 +313,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
     r->pending = true;
+    r->band0_rows = 0;  // set below when this call renders its frame in row bands
     // AUTO = wavefront: it beats the megakernel in every material mode (1080p
     // depth 8, 16 frames per launch, Msamples/s wavefront / megakernel: Lambert 725 / 414,
     // Dielectric 1239 / 758, Default 255 / 104).

@@ -124,3 +124,24 @@ def test_band_split_debug_pixel_both_bands():
         r.close()
     assert recs[True] == recs[False]
     assert all(len(g) > 0 for g in recs[True])
+
+
+def test_band_state_cleared_for_megakernel_calls():
+    """A banded call followed by a megakernel call: the second call's download must wait for its
+    own render, not for the earlier call's first-band event."""
+    from optixpathtracer_amd import scenes
+
+    sc = scenes.sphere_in_box("diffuse")
+    w, h = 96, 64
+    a = _renderer(sc, w, h, 6, 1, True)
+    b = _renderer(sc, w, h, 6, 1, True)
+    b.set_kernel(0)
+    a.Render(np.empty((h, w, 3), np.float32))  # banded wavefront frame 1
+    b.Render(np.empty((h, w, 3), np.float32))
+    a.set_kernel(0)  # megakernel from frame 2 on
+    for _ in range(3):
+        fa = a.Render(np.empty((h, w, 3), np.float32)).copy()
+        fb = b.Render(np.empty((h, w, 3), np.float32)).copy()
+        np.testing.assert_array_equal(fa, fb)
+    a.close()
+    b.close()
