@@ -689,7 +689,40 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     temp_bytes = std::max(temp_bytes, scan_bytes);
     PT_TRY(hipMalloc(&temp, temp_bytes > 0 ? temp_bytes : 16));
     PT_TRY(hipEventRecord(e0, stream));
-    {
+    if (in.builder == kBuilderSAH && n > 1) {
+        // host binned-SAH binary tree, then the same leaf gather and SAH-optimal collapse
+        std::vector<uint32_t> order;
+        std::vector<int2> hchild, hrange;
+        std::vector<float4> hbox;
+        sah_binary_tree(in.tri_host, n, order, hchild, hrange, hbox);
+        uint32_t* dfs = nullptr;
+        float4 *sbox = nullptr, *sleaf = nullptr, *spleaf = nullptr;
+        int2 *schild = nullptr, *srange = nullptr;
+        for (auto pr : {std::make_pair((void**)&dfs, sizeof(uint32_t) * (size_t)n),
+                        std::make_pair((void**)&schild, sizeof(int2) * (size_t)nbin),
+                        std::make_pair((void**)&srange, sizeof(int2) * (size_t)nbin),
+                        std::make_pair((void**)&sbox, sizeof(float4) * 2 * (size_t)nbin),
+                        std::make_pair((void**)&sleaf, sizeof(float4) * 2 * (size_t)n),
+                        std::make_pair((void**)&spleaf, sizeof(float4) * 2 * (size_t)n)}) {
+            PT_TRY(hipMalloc(pr.first, pr.second));
+            owned.push_back(*pr.first);
+        }
+        PT_TRY(hipMemcpyAsync(dfs, order.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice, stream));
+        PT_TRY(hipMemcpyAsync(schild, hchild.data(), sizeof(int2) * (size_t)nbin, hipMemcpyHostToDevice, stream));
+        PT_TRY(hipMemcpyAsync(srange, hrange.data(), sizeof(int2) * (size_t)nbin, hipMemcpyHostToDevice, stream));
+        PT_TRY(hipMemcpyAsync(sbox, hbox.data(), sizeof(float4) * 2 * (size_t)nbin, hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig,
+                           in.uv_orig, dfs, n, out.isect, out.shade, out.tuv, sleaf, spleaf);
+        PT_TRY(hipGetLastError());
+        PT_TRY(hipStreamSynchronize(stream));  // the host vectors go out of scope
+        B.child = schild;
+        B.range = srange;
+        B.box = sbox;
+        B.leafbox = sleaf;
+        B.pleaf = spleaf;
+        root = 0;
+    }
+    if (in.builder != kBuilderSAH || n <= 1) {
         float3 cmin = make_float3(in.cmin[0], in.cmin[1], in.cmin[2]);
         float ex = in.cmax[0] - in.cmin[0], ey = in.cmax[1] - in.cmin[1], ez = in.cmax[2] - in.cmin[2];
         float3 cinv = make_float3(ex > 0.0f ? 1.0f / ex : 0.0f, ey > 0.0f ? 1.0f / ey : 0.0f,
@@ -727,6 +760,8 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             B.pleaf = lb_pleaf;
             root = n > 1 ? 0 : ~0;
         }
+    }
+    {
         if (root >= 0) {  // SAH DP over the binary tree (n >= 2)
             PT_TRY(hipMalloc(&dp_parent, sizeof(int) * nbin));
             PT_TRY(hipMalloc(&dp_leafparent, sizeof(int) * n));

@@ -730,7 +730,8 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     for (int g = 0; g < opt.n_devices; ++g) devlist.push_back(opt.device_list ? opt.device_list[g] : opt.device + g);
     if (!devlist.empty()) opt.device = devlist[0];
     if (!valid_mode(opt.material_mode)) return fail(PT_ERR_INVALID, "pt_create: invalid material_mode");
-    if (opt.bvh_builder != PT_BVH_PLOC && opt.bvh_builder != PT_BVH_LBVH)
+    if (opt.bvh_builder != PT_BVH_AUTO && opt.bvh_builder != PT_BVH_PLOC && opt.bvh_builder != PT_BVH_LBVH &&
+        opt.bvh_builder != PT_BVH_SAH)
         return fail(PT_ERR_INVALID, "pt_create: invalid bvh_builder");
     if (opt.kernel != PT_KERNEL_MEGA && opt.kernel != PT_KERNEL_WAVEFRONT && opt.kernel != PT_KERNEL_AUTO)
         return fail(PT_ERR_INVALID, "pt_create: invalid kernel");
@@ -897,7 +898,9 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         in.nrm_orig = d_nrm_orig;
         in.uv_orig = d_uv_orig;
         in.n = (int)ntri;
-        in.builder = opt.bvh_builder == PT_BVH_LBVH ? kBuilderLBVH : kBuilderPLOC;
+        in.builder = opt.bvh_builder == PT_BVH_LBVH ? kBuilderLBVH : opt.bvh_builder == PT_BVH_PLOC ? kBuilderPLOC
+                                                                                                 : kBuilderSAH;
+        in.tri_host = tri.data();
         for (int a = 0; a < 3; ++a) {
             in.cmin[a] = cmin[a];
             in.cmax[a] = cmax[a];

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "pt_device.h"
 
@@ -16,10 +17,17 @@ struct BuildInput {
     const float4* uv_orig;   // 2 per triangle (uv0, uv1 | uv2, 0) or NULL (no textures)
     int n;
     float cmin[3], cmax[3];  // centroid bounds (Morton quantisation range)
-    int builder;             // kBuilderPLOC (default) or kBuilderLBVH
+    int builder;             // kBuilderPLOC (default), kBuilderLBVH or kBuilderSAH
+    const float4* tri_host;  // the same triangles on the host (kBuilderSAH builds there)
 };
 constexpr int kBuilderPLOC = 0;
 constexpr int kBuilderLBVH = 1;
+constexpr int kBuilderSAH = 2;
+
+// Host binned-SAH binary tree (pt_sah.cpp) in the GPU builders' layout: order = original triangle
+// per DFS leaf, child codes (>= 0 internal, ~k DFS leaf k), leaf ranges and plain boxes; root 0.
+void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std::vector<int2>& child,
+                     std::vector<int2>& range, std::vector<float4>& box);
 
 // BVH4 (collapsed LBVH) + triangle records in leaf order.
 struct BuildOutput {

@@ -85,7 +85,7 @@ class OptixRenderer:
     """Drop-in for `OptixRenderer` (OptixRenderer.h:8-110) backed by libptamd.so."""
 
     def __init__(self, ptx_path_or_none, model: Scene, device: int = 0, material_mode: int | None = None,
-                 kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC, devices=None):
+                 kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_AUTO, devices=None):
         """devices: None = the single `device`; a list of ordinals = one renderer over all of them
         (frame ids of render_frames split across the devices, RCCL-summed onto devices[0])."""
         # ptxPath is accepted for signature compatibility and ignored (no PTX on gfx950).
@@ -329,7 +329,7 @@ class OptixRenderer:
 
 
 def setup_renderer(scene: Scene, width: int, height: int, max_bounces: int, device: int = 0,
-                   kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_PLOC,
+                   kernel: int = capi.PT_KERNEL_AUTO, bvh_builder: int = capi.PT_BVH_AUTO,
                    devices=None) -> OptixRenderer:
     """The reference's main.cpp:95-113 sequence: construct, Resize, SetLights, SetMaxBounces, SetCamera."""
     r = OptixRenderer(None, scene, device=device, kernel=kernel, bvh_builder=bvh_builder, devices=devices)

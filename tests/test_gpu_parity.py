@@ -32,7 +32,7 @@ def diffuse_scene():
     return scenes.sphere_in_box("diffuse")
 
 
-@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
 def test_trace_closest_bit_exact(diffuse_scene, builder):
     from optixpathtracer_amd.renderer import setup_renderer
     from oracle.oracle import OracleScene
@@ -56,7 +56,7 @@ def test_trace_closest_bit_exact(diffuse_scene, builder):
     r.close()
 
 
-@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
 def test_trace_sponza_class_bit_exact(builder):
     """~250k triangles: deeper trees, many PLOC iterations, LDS-stack spills."""
     from optixpathtracer_amd import scenes
@@ -84,7 +84,7 @@ def test_trace_sponza_class_bit_exact(builder):
     o.close()
 
 
-@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
 def test_trace_two_triangles(builder):
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import OptixRenderer
@@ -102,7 +102,7 @@ def test_trace_two_triangles(builder):
     r.close()
 
 
-@pytest.mark.parametrize("builder", [0, 1], ids=["ploc", "lbvh"])
+@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
 def test_trace_empty_and_single_triangle(builder):
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import OptixRenderer

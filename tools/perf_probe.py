@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--fpl", default="8")
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--repeat", type=int, default=2)
-    ap.add_argument("--builders", default="0", help="0 = PLOC, 1 = LBVH")
+    ap.add_argument("--builders", default="0", help="0 = default (SAH), 1 = LBVH, 2 = SAH, 3 = PLOC")
     ap.add_argument("--streams", default="", help="wavefront streams to sweep (pt_set_wavefront_streams)")
     a = ap.parse_args()
     import os
