@@ -43,6 +43,14 @@ struct Box {
 #endif
 constexpr int kBins = PT_SAH_BINS;  // bins per axis of the split search
 
+// Bin of a centroid coordinate; NaN, below-range and infinite coordinates land in the end bins
+// (a float -> int conversion of NaN or of a value past INT_MAX is undefined).
+inline int bin_of(float c, float lo, float scale) {
+    const float f = (c - lo) * scale;
+    if (!(f > 0.0f)) return 0;
+    return f < (float)(kBins - 1) ? (int)f : kBins - 1;
+}
+
 }  // namespace
 
 // Binary tree over n >= 2 triangles: every internal node splits its range at the binned SAH
@@ -92,7 +100,7 @@ void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std
         float best_cost = FLT_MAX;
         for (int a = 0; a < 3; ++a) {
             const float ext = cb.hi[a] - cb.lo[a];
-            if (!(ext > 0.0f)) continue;
+            if (!(ext > 0.0f) || !std::isfinite(ext)) continue;
             const float scale = (float)kBins / ext;
             for (int b = 0; b < kBins; ++b) {
                 bin_box[a][b] = Box();
@@ -100,7 +108,7 @@ void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std
             }
             for (int k = it.begin; k < it.end; ++k) {
                 const uint32_t t = order[k];
-                const int b = std::min(kBins - 1, (int)((cen[3 * (size_t)t + a] - cb.lo[a]) * scale));
+                const int b = bin_of(cen[3 * (size_t)t + a], cb.lo[a], scale);
                 bin_box[a][b].grow(tb[t]);
                 bin_cnt[a][b]++;
             }
@@ -133,7 +141,7 @@ void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std
             const float scale = (float)kBins / (cb.hi[best_axis] - cb.lo[best_axis]);
             const float lo = cb.lo[best_axis];
             auto left = [&](uint32_t t) {
-                return std::min(kBins - 1, (int)((cen[3 * (size_t)t + best_axis] - lo) * scale)) <= best_split;
+                return bin_of(cen[3 * (size_t)t + best_axis], lo, scale) <= best_split;
             };
             mid = (int)(std::stable_partition(order.begin() + it.begin, order.begin() + it.end, left) - order.begin());
             if (mid == it.begin || mid == it.end) mid = it.begin + (it.end - it.begin) / 2;

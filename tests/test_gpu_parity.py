@@ -542,3 +542,33 @@ def test_fullhd_largest_batch_bit_identical(diffuse_scene, mode):
     assert sb["segments"] == sr["segments"]
     assert np.isfinite(ref).all()
     assert sr["samples"] == 1920 * 1080 * n
+
+
+@pytest.mark.parametrize("builder", [2, 3], ids=["sah", "ploc"])
+def test_degenerate_triangles_build_and_trace(builder):
+    """Zero-area, duplicate-centroid and NaN-vertex triangles among valid ones: every builder
+    finishes, and rays at the valid triangles hit them as the oracle says."""
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import OptixRenderer
+    from oracle.oracle import OracleScene
+
+    rng = np.random.default_rng(7)
+    v = rng.uniform(-1, 1, size=(300, 3)).astype(np.float32)
+    idx = np.arange(300, dtype=np.int32).reshape(100, 3)
+    v[3:6] = v[3]            # triangle 1: a point
+    v[6:9] = [[0, 0, 0], [1, 1, 1], [2, 2, 2]]  # triangle 2: a segment
+    v[9:12] = v[12:15] + np.float32(1e-7)  # triangles 3 and 4 nearly coincide
+    v[15] = np.nan           # triangle 5: a NaN vertex
+    mesh = scenes.Mesh(vertices=v, indices=idx, normals=np.tile(np.float32([0, 0, 1]), (300, 1)))
+    sc = scenes.Scene(meshes=[mesh], lights=np.zeros((0, 6), np.float32), camera_blender_pos=(0, 0, 0),
+                      camera_blender_rot=(0, 0, 0))
+    r = OptixRenderer(None, sc, bvh_builder=builder)
+    tri = v[idx[20:60]]
+    o = tri.mean(axis=1) + np.float32([0, 0, 3])
+    rays = np.concatenate([o, np.tile(np.float32([0, 0, -1]), (40, 1)), np.zeros((40, 1), np.float32),
+                           np.full((40, 1), 100, np.float32)], axis=1).astype(np.float32)
+    p, t, u, vv, b = r.trace_rays(rays)
+    r.close()
+    ref = OracleScene(sc).trace(rays)
+    np.testing.assert_array_equal(p, ref[0])
+    np.testing.assert_array_equal(t, ref[1])
