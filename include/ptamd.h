@@ -35,7 +35,7 @@ extern "C" {
 /* Render-kernel variants (all produce the same image). */
 #define PT_KERNEL_MEGA 0      /* one thread per pixel, frames looped in registers */
 #define PT_KERNEL_WAVEFRONT 1 /* wavefront: per-bounce kernels over SoA ray/hit queues, wave compaction */
-#define PT_BVH_AUTO 0          /* default: PT_BVH_SAH */
+#define PT_BVH_AUTO 0          /* default: PT_BVH_SAH up to 4 M triangles, PT_BVH_PLOC beyond */
 #define PT_BVH_LBVH 1          /* GPU Karras LBVH -> BVH4 (fastest build) */
 #define PT_BVH_SAH 2           /* host binned-SAH binary tree -> the GPU SAH-optimal BVH4 collapse: 13 %
                                   fewer node visits per ray than PLOC; 19 ms at 35k,

@@ -340,7 +340,7 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // moves the camera every frame gets): its rows split into two bands, one per stream, so
         // each band's kernels fill the other's SIMT tails.  Every pixel's path depends only on its
         // pixel and frame id, so the image is the same bit for bit.
-        const bool bands = n == 1 && r->band_split && r->height > 1;
+        const bool bands = n == 1 && r->band_split && r->height >= 16;  // both bands non-empty
         int ns = std::max(1, std::min(r->wf_streams, bands ? 2 : nbatch));
         for (int k = 0; k < ns; ++k) {
             WFState& w = k ? r->xwf[k] : r->wf;
@@ -898,8 +898,14 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         in.nrm_orig = d_nrm_orig;
         in.uv_orig = d_uv_orig;
         in.n = (int)ntri;
-        in.builder = opt.bvh_builder == PT_BVH_LBVH ? kBuilderLBVH : opt.bvh_builder == PT_BVH_PLOC ? kBuilderPLOC
-                                                                                                 : kBuilderSAH;
+        // AUTO: the host SAH tree (fewest node visits) up to 4 M triangles (≈ 0.1 s per 250 k on one
+        // host thread), the GPU PLOC tree beyond
+        constexpr size_t kAutoSahMaxTris = size_t(1) << 22;
+        in.builder = opt.bvh_builder == PT_BVH_LBVH   ? kBuilderLBVH
+                     : opt.bvh_builder == PT_BVH_PLOC ? kBuilderPLOC
+                     : opt.bvh_builder == PT_BVH_SAH  ? kBuilderSAH
+                     : ntri <= kAutoSahMaxTris        ? kBuilderSAH
+                                                      : kBuilderPLOC;
         in.tri_host = tri.data();
         for (int a = 0; a < 3; ++a) {
             in.cmin[a] = cmin[a];
