@@ -477,6 +477,9 @@ def main():
                 "frames_per_launch": args.frames_per_launch,
                 "parallelism": f"spp-shard x{world}",
                 "lbvh_build_ms": round(bvh_ms, 3),
+                # pt_options.bvh_builder = PT_BVH_AUTO: the host binned-SAH binary tree (<= 4 M
+                # triangles) collapsed to BVH4 on the GPU; the time above covers both
+                "bvh_builder": "auto (host binned SAH + GPU SAH-optimal BVH4 collapse)",
                 "primary_dedup": args.kernel != 0,
             },
             # one extra step with pt_set_primary_dedup(0): each frame traces its own copy of the
