@@ -28,6 +28,13 @@ constexpr int kBuilderSAH = 2;
 // per DFS leaf, child codes (>= 0 internal, ~k DFS leaf k), leaf ranges and plain boxes; root 0.
 void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std::vector<int2>& child,
                      std::vector<int2>& range, std::vector<float4>& box);
+// Insertion-based optimisation of that tree in place (pt_sah.cpp); returns the relative cost cut.
+// PT_SAH_REINSERT = the most rounds kBuilderSAH runs (0: off).
+#ifndef PT_SAH_REINSERT
+#define PT_SAH_REINSERT 16
+#endif
+double sah_reinsert(std::vector<uint32_t>& order, std::vector<int2>& child, std::vector<int2>& range,
+                    std::vector<float4>& box, const float4* tri, int rounds);
 
 // BVH4 (collapsed LBVH) + triangle records in leaf order.
 struct BuildOutput {

