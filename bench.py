@@ -290,6 +290,7 @@ def main():
     # batch's kernels and its event window is longer than its solo run.  One more step on a
     # single stream gives the trace kernels' solo launch time (roofline.single_stream).
     single = None
+    s1_all_ms = None  # single-stream mean over all trace launches (vmem rate)
     if args.kernel != 0 and not args.no_dedup_check and args.wavefront_streams > 1:
         r.set_wavefront_streams(1)
         r.stats_reset()
@@ -304,10 +305,14 @@ def main():
         e2 = time.perf_counter() - t2
         s1 = r.stats()
         if s1["trace_kernel_launches"] > 0:
-            l1 = int(s1["trace_kernel_launches"])
-            ms1 = s1["trace_kernel_ms"] / l1
-            ach1 = s1["trace_kernel_bytes"] / l1 / (ms1 / 1e3) / 1e9
+            # the dominant trace kernel alone: k_trace_pair in the fused modes, k_extend otherwise
+            pair1 = s1["pair_kernel_launches"] > 0
+            l1 = int(s1["pair_kernel_launches"] if pair1 else s1["trace_kernel_launches"])
+            ms1 = (s1["pair_kernel_ms"] if pair1 else s1["trace_kernel_ms"]) / l1
+            ach1 = (s1["pair_kernel_bytes"] if pair1 else s1["trace_kernel_bytes"]) / l1 / (ms1 / 1e3) / 1e9
+            s1_all_ms = s1["trace_kernel_ms"] / max(1, s1["trace_kernel_launches"])
             single = {"value": round(args.width * args.height * per_step_spp / e2 / 1e6, 3),
+                      "kernel": "k_trace_pair" if pair1 else "k_extend",
                       "avg_launch_ms": round(ms1, 4), "achieved": round(ach1, 2),
                       "frac": round(ach1 / HBM_PEAK_GBPS, 5), "launches": l1,
                       "shade_avg_launch_ms": round(s1["shade_kernel_ms"] / max(1, s1["shade_kernel_launches"]), 4),
@@ -331,10 +336,15 @@ def main():
         fused = scene.material_mode in (1, 2, 3)
         vmem_line = valu_line = trace_line = None
         if st["trace_kernel_launches"] > 0:
-            launches = int(st["trace_kernel_launches"])
-            t_bytes = st["trace_kernel_bytes"] / launches
-            t_s = st["trace_kernel_ms"] / 1e3 / launches
-            trace_line = {"kernel": "k_extend+k_trace_pair" if fused else "k_extend", "launches": launches,
+            # per kernel: k_trace_pair's own launches in the fused modes
+            # (the batch's one k_extend is excluded), k_extend in Default / Layered
+            pair = fused and st["pair_kernel_launches"] > 0
+            launches = int(st["pair_kernel_launches"] if pair else st["trace_kernel_launches"])
+            t_bytes = (st["pair_kernel_bytes"] if pair else st["trace_kernel_bytes"]) / launches
+            t_s = (st["pair_kernel_ms"] if pair else st["trace_kernel_ms"]) / 1e3 / launches
+            # all trace launches (k_extend + k_trace_pair): the denominator of the lane-load rate below
+            all_s = st["trace_kernel_ms"] / 1e3 / int(st["trace_kernel_launches"])
+            trace_line = {"kernel": "k_trace_pair" if pair else "k_extend", "launches": launches,
                           "avg_launch_ms": round(t_s * 1e3, 4), "bytes_per_launch": int(t_bytes),
                           "achieved": round(t_bytes / t_s / 1e9, 2), "frac": round(t_bytes / t_s / 1e9 / HBM_PEAK_GBPS, 5)}
             if trav and trav["trace_kernel_launches"] > 0:
@@ -347,9 +357,10 @@ def main():
                 ext_rays = trav["rays"] - trav["shadow_rays"]
                 loads = (NODE_LOADS * g_nodes + TRI_LOADS * trav["tri_tests"] + 2 * ext_rays
                          + 3 * trav["shadow_rays"]) / tl
-                ach_v = loads / t_s
+                ach_v = loads / all_s  # lane loads of all trace launches over their summed time
                 vmem_line = {
-                    "unit": "16-B lane loads/s", "lane_loads_per_launch": round(loads),
+                    "unit": "16-B lane loads/s", "kernels": "k_extend + k_trace_pair (aggregate rate)",
+                    "lane_loads_per_launch": round(loads),
                     "achieved": round(ach_v / 1e9, 2), "ceiling": round(VMEM_LOADS_PER_S / 1e9, 1),
                     "frac": round(ach_v / VMEM_LOADS_PER_S, 4),
                     "ceiling_def": "1 line per CU-cycle x 256 CUs x 2.4 GHz (tools/td_probe.hip)",
@@ -358,8 +369,8 @@ def main():
                     "tri_tests_per_ray": round(trav["tri_tests"] / max(1, trav["rays"]), 3),
                     "node_lane_utilisation": round(trav["nodes_visited"] / max(1, 64 * trav["wave_node_steps"]), 4),
                 }
-                if single:
-                    sv = loads / (single["avg_launch_ms"] / 1e3)
+                if single and s1_all_ms:
+                    sv = loads / (s1_all_ms / 1e3)
                     vmem_line["single_stream"] = {"achieved": round(sv / 1e9, 2), "frac": round(sv / VMEM_LOADS_PER_S, 4)}
         if fused and trace_line:
             # Lambert / Conductor / Dielectric: the trace kernels are the dominant kernels (k_extend
@@ -367,11 +378,12 @@ def main():
             # launch bracketed by its own HIP event pair on the stream it runs on
             dom = trace_line["kernel"]
             launches = trace_line["launches"]
-            per_launch_bytes = st["trace_kernel_bytes"] / launches
-            avg_launch_s = st["trace_kernel_ms"] / 1e3 / launches
-            bytes_def = ("48 B per traced ray: the 32-B ray record read and one 16-B result, the hit record of an "
-                         "extension ray (one per pixel at bounce 0, shared by the pixel's frames of the batch) or "
-                         "the deferred radiance add of an unoccluded shadow ray")
+            per_launch_bytes = trace_line["bytes_per_launch"]
+            avg_launch_s = trace_line["avg_launch_ms"] / 1e3
+            bytes_def = ("48 B per traced ray of one k_trace_pair launch (the shadow rays of bounce b and the "
+                         "extension rays of bounce b+1 of a 64-frame batch): the 32-B ray record read and one 16-B "
+                         "result, the hit record of an extension ray or the deferred radiance add of an "
+                         "unoccluded shadow ray")
         elif st["shade_kernel_launches"] > 0:
             # Default / Layered: k_shade_nee (the stochastic layered NEE eval) takes 53-60 % of a frame
             # (DESIGN.md §8); its bound is VALU issue (roofline.valu), its HBM figure is reported too
@@ -448,6 +460,24 @@ def main():
                     valu_line = {**fig, "sources_sha": sha}
                 else:
                     pmc_stale["valu"] = {**fig, "sources_sha": nd.get("sources_sha"), "stale": True}
+        # The unit that binds the dominant kernel.  `bound` stays "hbm": the
+        # contract's roofline (achieved / peak in GB/s) is HBM; this names what the counters show.
+        if dom == "k_trace_pair":
+            binding = {"unit": "vector memory path (TA/TD): latency of each step's dependent load chain",
+                       "frac": (vmem_line or {}).get("single_stream", {}).get("frac") or (vmem_line or {}).get("frac"),
+                       "frac_def": "16-B lane loads/s of the trace launches (single stream) over one line per CU-cycle "
+                                   "(roofline.vmem)",
+                       "td_busy": (vmem or {}).get("td_busy"), "ta_busy": (vmem or {}).get("ta_busy"),
+                       "hbm_frac_single_stream": (single or {}).get("frac")}
+        elif dom == "k_shade_nee":
+            vl = valu_line or {}
+            ef = (round(vl["issue_frac"] * vl["lane_utilisation"], 4)
+                  if vl.get("issue_frac") and vl.get("lane_utilisation") else None)
+            binding = {"unit": "VALU", "frac": ef,
+                       "frac_def": "VALU issue fraction x lane utilisation (roofline.valu, PMC)",
+                       "issue_frac": vl.get("issue_frac"), "lane_utilisation": vl.get("lane_utilisation")}
+        else:
+            binding = None
         out = {
             "metric": "Msamples/sec at 1920x1080, max-depth 8; MSE vs reference",
             "value": round(value, 3),
@@ -500,6 +530,12 @@ def main():
                 "bytes_def": bytes_def,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "launches": launches,
+                # the timed region alternates batches over two streams: a launch's event window
+                # includes time it shares the GPU with the other stream's kernels (single_stream
+                # gives the same kernel alone)
+                "window": ("timed region, two wavefront streams (concurrent launch windows)"
+                           if args.wavefront_streams > 1 else "timed region, one stream"),
+                "binding": binding,
                 "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
                 # SURVEY.md §8(d) whole-path figure: (segments*396 + samples*12) / render time
                 "pipeline_gbps": round(alg_bytes / max(kernel_s, 1e-9) / 1e9, 2),

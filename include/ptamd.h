@@ -157,6 +157,16 @@ typedef struct pt_stats {
        (frames_rendered_ahead - frames_served_ahead of them at most). */
     uint64_t frames_rendered_ahead;
     uint64_t frames_served_ahead;
+    /* look-ahead batches cancelled because the render state changed while they were in flight
+       (their frames count in frames_rendered_ahead, but they stopped early) */
+    uint64_t look_ahead_cancelled;
+    /* the k_trace_pair launches alone (fused modes: every timed trace launch but the batch's
+       k_extend), per kernel for the roofline: event time, launches, rays, algorithmic bytes
+       (48 B per ray); included in trace_kernel_* as well */
+    double pair_kernel_ms;
+    uint64_t pair_kernel_launches;
+    uint64_t pair_kernel_rays;
+    uint64_t pair_kernel_bytes;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;

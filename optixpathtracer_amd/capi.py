@@ -131,6 +131,11 @@ class pt_stats(C.Structure):
         ("shade_kernel_items", C.c_uint64),
         ("frames_rendered_ahead", C.c_uint64),
         ("frames_served_ahead", C.c_uint64),
+        ("look_ahead_cancelled", C.c_uint64),
+        ("pair_kernel_ms", C.c_double),
+        ("pair_kernel_launches", C.c_uint64),
+        ("pair_kernel_rays", C.c_uint64),
+        ("pair_kernel_bytes", C.c_uint64),
     ]
 
 

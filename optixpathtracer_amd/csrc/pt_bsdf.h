@@ -25,7 +25,7 @@ __device__ __forceinline__ void disk_polar(uint32_t& seed, float& px, float& py)
     const float pi = (float)3.14159265359;
     float u0 = rnd(seed);
     float u1 = rnd(seed);
-    float r = sqrtf(u0);
+    float r = fsqrt(u0);
     float theta = 2.0f * pi * u1;
     float st, ct;
     pt_sincosf(theta, st, ct);  // cosf / sinf (pt_math.h: bit-identical to the oracle)
@@ -47,10 +47,10 @@ __device__ __forceinline__ void disk_concentric(uint32_t& seed, float& dx, float
     float theta, r;
     if (gabs(ox) > gabs(oy)) {
         r = ox;
-        theta = PiOver4 * (oy / ox);
+        theta = PiOver4 * fdiv(oy, ox);
     } else {
         r = oy;
-        theta = PiOver2 - PiOver4 * (ox / oy);
+        theta = PiOver2 - PiOver4 * fdiv(ox, oy);
     }
     float st, ct;
     pt_sincosf(theta, st, ct);
@@ -62,15 +62,15 @@ __device__ __forceinline__ void disk_concentric(uint32_t& seed, float& dx, float
 __device__ __forceinline__ float cos2_theta(f3 w) { return sqr(w.z); }
 __device__ __forceinline__ float abs_cos_theta(f3 w) { return gabs(w.z); }
 __device__ __forceinline__ float sin2_theta(f3 w) { return gmax(0.0f, 1.0f - cos2_theta(w)); }
-__device__ __forceinline__ float sin_theta(f3 w) { return sqrtf(sin2_theta(w)); }
-__device__ __forceinline__ float tan2_theta(f3 w) { return sin2_theta(w) / cos2_theta(w); }
+__device__ __forceinline__ float sin_theta(f3 w) { return fsqrt(sin2_theta(w)); }
+__device__ __forceinline__ float tan2_theta(f3 w) { return fdiv(sin2_theta(w), cos2_theta(w)); }
 __device__ __forceinline__ float cos_phi(f3 w) {
     float s = sin_theta(w);
-    return (s == 0.0f) ? 1.0f : gclamp(w.x / s, -1.0f, 1.0f);
+    return (s == 0.0f) ? 1.0f : gclamp(fdiv(w.x, s), -1.0f, 1.0f);
 }
 __device__ __forceinline__ float sin_phi(f3 w) {
     float s = sin_theta(w);
-    return (s == 0.0f) ? 0.0f : gclamp(w.y / s, -1.0f, 1.0f);
+    return (s == 0.0f) ? 0.0f : gclamp(fdiv(w.y, s), -1.0f, 1.0f);
 }
 __device__ __forceinline__ bool same_hemisphere(f3 w, f3 wp) { return w.z * wp.z > 0.0f; }
 
@@ -81,21 +81,21 @@ __device__ __forceinline__ float tr_D(f3 wm, float alpha) {
     if (isinf(t2)) return 0.0f;
     float cos4 = sqr(cos2_theta(wm));
     if (cos4 < 1e-16f) return 0.0f;
-    float e = t2 * (sqr(cos_phi(wm) / alpha) + sqr(sin_phi(wm) / alpha));
-    return 1.0f / (pi * alpha * alpha * cos4 * sqr(1.0f + e));
+    float e = t2 * (sqr(fdiv(cos_phi(wm), alpha)) + sqr(fdiv(sin_phi(wm), alpha)));
+    return frcp(pi * alpha * alpha * cos4 * sqr(1.0f + e));
 }
 __device__ __forceinline__ float tr_lambda(f3 w, float alpha) {
     float t2 = tan2_theta(w);
     if (isinf(t2)) return 0.0f;
     float a2 = sqr(cos_phi(w) * alpha) + sqr(sin_phi(w) * alpha);
-    return (sqrtf(1.0f + a2 * t2) - 1.0f) / 2.0f;
+    return (fsqrt(1.0f + a2 * t2) - 1.0f) / 2.0f;  // / 2: an exact multiply
 }
 __device__ __forceinline__ float tr_G(f3 wo, f3 wi, float alpha) {
-    return 1.0f / (1.0f + tr_lambda(wo, alpha) + tr_lambda(wi, alpha));
+    return frcp(1.0f + tr_lambda(wo, alpha) + tr_lambda(wi, alpha));
 }
-__device__ __forceinline__ float tr_G1(f3 w, float alpha) { return 1.0f / (1.0f + tr_lambda(w, alpha)); }
+__device__ __forceinline__ float tr_G1(f3 w, float alpha) { return frcp(1.0f + tr_lambda(w, alpha)); }
 __device__ __forceinline__ float tr_pdf(f3 w, f3 wm, float alpha) {   // D(w, wm): :81-88
-    return tr_G1(w, alpha) / abs_cos_theta(w) * tr_D(wm, alpha) * abs_dot(w, wm);
+    return fdiv(tr_G1(w, alpha), abs_cos_theta(w)) * tr_D(wm, alpha) * abs_dot(w, wm);
 }
 // Trowbridge-Reitz quantities of one direction w that every sample or evaluation with w as
 // the outgoing direction recomputes: tr_sample_wm's hemisphere frame, Lambda(w) and
@@ -109,7 +109,7 @@ struct TRDir {
 };
 __device__ __forceinline__ void tr_dir_lam(TRDir& p, f3 w, float alpha) {
     p.lam = tr_lambda(w, alpha);
-    p.g1c = (1.0f / (1.0f + p.lam)) / abs_cos_theta(w);
+    p.g1c = fdiv(frcp(1.0f + p.lam), abs_cos_theta(w));
 }
 __device__ __forceinline__ void tr_dir_frame(TRDir& p, f3 w, float alpha) {  // Microfacet.h:90-98
     f3 wh = normalize(mk(alpha * w.x, alpha * w.y, w.z));
@@ -122,10 +122,10 @@ __device__ __forceinline__ f3 tr_sample_wm_dir(uint32_t& seed, const TRDir& p, f
     const f3 wh = p.wh, T1 = p.T1, T2 = p.T2;
     float px, py;
     disk_polar(seed, px, py);
-    float h = sqrtf(1.0f - sqr(px));
+    float h = fsqrt(1.0f - sqr(px));
     float x = (1.0f + wh.z) / 2.0f;
     py = (1.0f - x) * h + x * py;
-    float pz = sqrtf(gmax(0.0f, 1.0f - (sqr(px) + sqr(py))));
+    float pz = fsqrt(gmax(0.0f, 1.0f - (sqr(px) + sqr(py))));
     f3 nh = mk(px * T1.x + py * T2.x + pz * wh.x, px * T1.y + py * T2.y + pz * wh.y,
                px * T1.z + py * T2.z + pz * wh.z);
     return normalize(mk(alpha * nh.x, alpha * nh.y, gmax(1e-6f, nh.z)));
@@ -146,14 +146,14 @@ __device__ __forceinline__ cpx c_mul(cpx a, cpx b) {
     return cpx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
 __device__ __forceinline__ cpx c_div(cpx a, cpx z) {
-    float scale = 1.0f / (z.re * z.re + z.im * z.im);
+    float scale = frcp(z.re * z.re + z.im * z.im);
     return cpx{scale * (a.re * z.re + a.im * z.im), scale * (a.im * z.re - a.re * z.im)};
 }
 __device__ __forceinline__ float c_norm(cpx z) { return z.re * z.re + z.im * z.im; }
 __device__ __forceinline__ cpx c_sqrt(cpx z) {
-    float n = sqrtf(c_norm(z));
-    float t1 = sqrtf(0.5f * (n + gabs(z.re)));
-    float t2 = 0.5f * z.im / t1;
+    float n = fsqrt(c_norm(z));
+    float t1 = fsqrt(0.5f * (n + gabs(z.re)));
+    float t2 = fdiv(0.5f * z.im, t1);
     if (n == 0.0f) return cpx{0.0f, 0.0f};
     if (z.re >= 0.0f) return cpx{t1, t2};
     return cpx{gabs(t2), copysignf(t1, z.im)};
@@ -173,7 +173,7 @@ __device__ __forceinline__ float fresnel_complex1(float cos_i, float refl) {  //
     float r = gclamp(refl, 0.0f, 0.9999f);
     float om = 1.0f - r;
     om = om > 0.0f ? om : 0.0f;
-    float k = 2.0f * sqrtf(r) / sqrtf(om);
+    float k = fdiv(2.0f * fsqrt(r), fsqrt(om));
     return fr_complex(cos_i, cpx{1.0f, k});
 }
 __device__ __forceinline__ f3 fresnel_complex(float cos_i, f3 refl) {
@@ -192,7 +192,7 @@ __device__ __forceinline__ f3 conductor_f(f3 albedo, float roughness, f3 wo, f3 
     f3 F = fresnel_complex(abs_dot(wo, wm), albedo);
     float D = tr_D(wm, alpha), G = tr_G(wo, wi, alpha);
     float den = 4.0f * ci * co;
-    return mk(D * F.x * G / den, D * F.y * G / den, D * F.z * G / den);
+    return mk(fdiv(D * F.x * G, den), fdiv(D * F.y * G, den), fdiv(D * F.z * G, den));
 }
 __device__ __forceinline__ bool conductor_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo,
                                                  BSample& s) {  // :122-190
@@ -200,7 +200,7 @@ __device__ __forceinline__ bool conductor_sample(uint32_t& seed, f3 albedo, floa
     if (alpha < 1e-3f) {
         f3 wi = mk(-wo.x, -wo.y, wo.z);
         float ac = abs_cos_theta(wi);
-        s.color = fresnel_complex(ac, albedo) / ac;
+        s.color = fresnel_complex(ac, albedo) / ac;  // f3 / float: fdiv per channel
         s.dir = wi;
         s.pdf = 1.0f;
         s.refl = true;
@@ -213,13 +213,13 @@ __device__ __forceinline__ bool conductor_sample(uint32_t& seed, f3 albedo, floa
     float d2 = 2.0f * dot(wo, wm);
     f3 wi = (-wo) + d2 * wm;
     if (!same_hemisphere(wo, wi)) return false;
-    float pdf = tr_pdf(wo, wm, alpha) / (4.0f * abs_dot(wo, wm));
+    float pdf = fdiv(tr_pdf(wo, wm, alpha), 4.0f * abs_dot(wo, wm));
     float co = abs_cos_theta(wo), ci = abs_cos_theta(wi);
     if (ci == 0.0f || co == 0.0f) return false;
     f3 F = fresnel_complex(abs_dot(wo, wm), albedo);
     float D = tr_D(wm, alpha), G = tr_G(wo, wi, alpha);
     float den = 4.0f * ci * co;
-    s.color = mk(D * F.x * G / den, D * F.y * G / den, D * F.z * G / den);
+    s.color = mk(fdiv(D * F.x * G, den), fdiv(D * F.y * G, den), fdiv(D * F.z * G, den));
     s.dir = wi;
     s.pdf = pdf;
     s.refl = true;
@@ -238,7 +238,7 @@ __device__ __forceinline__ bool lambert_sample(uint32_t& seed, f3 albedo, bool r
     if (!reflection) return false;
     float dx, dy;
     disk_concentric(seed, dx, dy);
-    float z = sqrtf(gmax(0.0f, 1.0f - sqr(dx) - sqr(dy)));
+    float z = fsqrt(gmax(0.0f, 1.0f - sqr(dx) - sqr(dy)));
     f3 d = mk(dx, dy, z);
     if (d.z < 0.0f) d.z *= -1.0f;
     d = normalize(d);
@@ -264,11 +264,11 @@ __device__ __forceinline__ float fresnel_dielectric(float cos_i, float ior) {  /
         cos_i = -cos_i;
     }
     float sin2i = 1.0f - sqr(cos_i);
-    float sin2t = sin2i / sqr(ior);
+    float sin2t = fdiv(sin2i, sqr(ior));
     if (sin2t >= 1.0f) return 1.0f;
-    float cost = sqrtf(1.0f - sin2t);
-    float r_parl = (ior * cos_i - cost) / (ior * cos_i + cost);
-    float r_perp = (cos_i - ior * cost) / (cos_i + ior * cost);
+    float cost = fsqrt(1.0f - sin2t);
+    float r_parl = fdiv(ior * cos_i - cost, ior * cos_i + cost);
+    float r_perp = fdiv(cos_i - ior * cost, cos_i + ior * cost);
     return (sqr(r_parl) + sqr(r_perp)) / 2.0f;
 }
 __device__ __forceinline__ bool refract(f3 wi, f3 n, float eta, float& etap, f3& wt) {  // :68-92
@@ -279,11 +279,11 @@ __device__ __forceinline__ bool refract(f3 wi, f3 n, float eta, float& etap, f3&
         n = -n;
     }
     float sin2i = gmax(0.0f, 1.0f - sqr(cos_i));
-    float sin2t = sin2i / sqr(eta);
+    float sin2t = fdiv(sin2i, sqr(eta));
     if (sin2t >= 1.0f) return false;
-    float cost = sqrtf(1.0f - sin2t);
-    float k = cos_i / eta - cost;
-    wt = ((-wi) / eta) + k * n;
+    float cost = fsqrt(1.0f - sin2t);
+    float k = fdiv(cos_i, eta) - cost;
+    wt = ((-wi) / eta) + k * n;  // f3 / float: fdiv per channel
     etap = eta;
     return true;
 }
@@ -305,10 +305,10 @@ __device__ __forceinline__ float dielectric_f(float roughness, f3 wo, f3 wi, int
     wm = faceforward_z(wm);
     if (dot(wm, wi) * ci < 0.0f || dot(wm, wo) * co < 0.0f) return 0.0f;
     float F = fresnel_dielectric(dot(wo, wm), eta);
-    if (reflect) return tr_D(wm, alpha) * tr_G(wo, wi, alpha) * F / fabsf(4.0f * ci * co);
-    float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap) * ci * co;
-    float ft = tr_D(wm, alpha) * (1.0f - F) * tr_G(wo, wi, alpha) * fabsf(dot(wi, wm) * dot(wo, wm) / denom);
-    if (mode == kRadiance) ft /= sqr(etap);
+    if (reflect) return fdiv(tr_D(wm, alpha) * tr_G(wo, wi, alpha) * F, fabsf(4.0f * ci * co));
+    float denom = sqr(dot(wi, wm) + fdiv(dot(wo, wm), etap)) * ci * co;
+    float ft = tr_D(wm, alpha) * (1.0f - F) * tr_G(wo, wi, alpha) * fabsf(fdiv(dot(wi, wm) * dot(wo, wm), denom));
+    if (mode == kRadiance) ft = fdiv(ft, sqr(etap));
     return ft;
 }
 // Dielectric.h:146-288 with the wo-only Trowbridge-Reitz terms taken from `p` (a full TRDir of
@@ -325,12 +325,12 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
         if (!reflection) pr = 0.0f;
         if (!transmission) pt = 0.0f;
         if (pr == 0.0f && pt == 0.0f) return false;
-        if (uc < pr / (pr + pt)) {
+        if (uc < fdiv(pr, pr + pt)) {
             f3 wi = mk(-wo.x, -wo.y, wo.z);
-            float fr = R / abs_cos_theta(wi);
+            float fr = fdiv(R, abs_cos_theta(wi));
             s.color = mk(fr, fr, fr);
             s.dir = wi;
-            s.pdf = pr / (pr + pt);
+            s.pdf = fdiv(pr, pr + pt);
             s.refl = true;
             s.trans = false;
             s.spec = true;
@@ -339,11 +339,11 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
         f3 wi;
         float etap;
         if (!refract(wo, mk(0.0f, 0.0f, 1.0f), eta, etap, wi)) return false;
-        float ft = T / abs_cos_theta(wi);
-        if (mode == kRadiance) ft /= sqr(etap);
+        float ft = fdiv(T, abs_cos_theta(wi));
+        if (mode == kRadiance) ft = fdiv(ft, sqr(etap));
         s.color = mk(ft, ft, ft);
         s.dir = wi;
-        s.pdf = pt / (pr + pt);
+        s.pdf = fdiv(pt, pr + pt);
         s.refl = false;
         s.trans = true;
         s.spec = true;
@@ -361,7 +361,7 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
     // D(wm) and Lambda(wi) and end in the same divisions, so they are computed once here, on the
     // lane's own wi and with each division's operands selected per lobe: every value is the one
     // its branch computes, with one copy of the expensive terms instead of two.
-    const bool refl = uc < pr / (pr + pt);
+    const bool refl = uc < fdiv(pr, pr + pt);
     const f3 I = -wo;  // glm::reflect(I, N) = I - N*dot(N,I)*2
     const float dr = dot(wm, I);
     const f3 wr = mk(I.x - wm.x * dr * 2.0f, I.y - wm.y * dr * 2.0f, I.z - wm.z * dr * 2.0f);
@@ -372,15 +372,15 @@ __device__ __forceinline__ bool dielectric_sample_dir(uint32_t& seed, float roug
     if (refl ? !same_hemisphere(wo, wi) : (tir || same_hemisphere(wo, wi) || wi.z == 0.0f)) return false;
     const float etap = refl ? 1.0f : etap_t;
     const float D = tr_D(wm, alpha);
-    const float G = 1.0f / (1.0f + p.lam + tr_lambda(wi, alpha));
+    const float G = frcp(1.0f + p.lam + tr_lambda(wi, alpha));
     const float adw = abs_dot(wo, wm);
     const float A = p.g1c * D * adw;
-    const float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);            // transmission only
-    const float q1 = (refl ? A : abs_dot(wi, wm)) / (refl ? 4.0f * adw : denom);  // A/(4|wo.wm|) | dwm_dwi
-    const float pdf = (refl ? q1 * pr : A * q1 * pt) / (pr + pt);
-    const float q2 = (refl ? D * G * R : dot(wi, wm) * dot(wo, wm)) / (refl ? 4.0f * wi.z * wo.z : wi.z * wo.z * denom);
+    const float denom = sqr(dot(wi, wm) + fdiv(dot(wo, wm), etap));            // transmission only
+    const float q1 = fdiv(refl ? A : abs_dot(wi, wm), refl ? 4.0f * adw : denom);  // A/(4|wo.wm|) | dwm_dwi
+    const float pdf = fdiv(refl ? q1 * pr : A * q1 * pt, pr + pt);
+    const float q2 = fdiv(refl ? D * G * R : dot(wi, wm) * dot(wo, wm), refl ? 4.0f * wi.z * wo.z : wi.z * wo.z * denom);
     float f = refl ? q2 : T * D * G * fabsf(q2);
-    const float fd = f / sqr(etap);
+    const float fd = fdiv(f, sqr(etap));
     if (!refl && mode == kRadiance) f = fd;
     s.color = mk(f, f, f);
     s.dir = wi;
@@ -419,10 +419,10 @@ __device__ __forceinline__ float dielectric_pdf(float roughness, f3 wo, f3 wi, b
     if (!reflection) pr = 0.0f;
     if (!transmission) pt = 0.0f;
     if (pr == 0.0f && pt == 0.0f) return 0.0f;
-    if (reflect) return tr_pdf(wo, wm, alpha) / (4.0f * abs_dot(wo, wm)) * pr / (pr + pt);
-    float denom = sqr(dot(wi, wm) + dot(wo, wm) / etap);
-    float dwm_dwi = abs_dot(wi, wm) / denom;
-    return tr_pdf(wo, wm, alpha) * dwm_dwi * pt / (pr + pt);
+    if (reflect) return fdiv(fdiv(tr_pdf(wo, wm, alpha), 4.0f * abs_dot(wo, wm)) * pr, pr + pt);
+    float denom = sqr(dot(wi, wm) + fdiv(dot(wo, wm), etap));
+    float dwm_dwi = fdiv(abs_dot(wi, wm), denom);
+    return fdiv(tr_pdf(wo, wm, alpha) * dwm_dwi * pt, pr + pt);
 }
 
 // dielectric_f and dielectric_pdf at the same (wo, wi) in one pass: the half vector, the
@@ -452,7 +452,7 @@ __device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, con
     if (dot(wm, wi) * ci < 0.0f || dot(wm, wo) * co < 0.0f) return;
     const float F = fresnel_dielectric(dot(wo, wm), eta);
     const float D = tr_D(wm, alpha);
-    const float G = 1.0f / (1.0f + po.lam + lam_i);
+    const float G = frcp(1.0f + po.lam + lam_i);
     const float tp = po.g1c * D * abs_dot(wo, wm);
     float fv, pv;
     // reflection and transmission in one sequence (lanes of a wave disagree on `reflect`): each
@@ -461,13 +461,13 @@ __device__ __forceinline__ void dielectric_f_pdf_dir(float roughness, f3 wo, con
     float pr = R, pt = T;
     if (!reflection) pr = 0.0f;
     if (!transmission) pt = 0.0f;
-    const float s2 = sqr(dot(wi, wm) + dot(wo, wm) / etap);  // transmission only
-    const float qf = (reflect ? D * G * F : dot(wi, wm) * dot(wo, wm)) / (reflect ? fabsf(4.0f * ci * co) : s2 * ci * co);
+    const float s2 = sqr(dot(wi, wm) + fdiv(dot(wo, wm), etap));  // transmission only
+    const float qf = fdiv(reflect ? D * G * F : dot(wi, wm) * dot(wo, wm), reflect ? fabsf(4.0f * ci * co) : s2 * ci * co);
     fv = reflect ? qf : D * (1.0f - F) * G * fabsf(qf);
-    const float fd = fv / sqr(etap);
+    const float fd = fdiv(fv, sqr(etap));
     if (!reflect && mode == kRadiance) fv = fd;
-    const float qp = (reflect ? tp : abs_dot(wi, wm)) / (reflect ? 4.0f * abs_dot(wo, wm) : s2);
-    pv = (reflect ? qp * pr : tp * qp * pt) / (pr + pt);
+    const float qp = fdiv(reflect ? tp : abs_dot(wi, wm), reflect ? 4.0f * abs_dot(wo, wm) : s2);
+    pv = fdiv(reflect ? qp * pr : tp * qp * pt, pr + pt);
     if (pr == 0.0f && pt == 0.0f) pv = 0.0f;
     f = f_ok ? fv : 0.0f;
     pdf = p_ok ? pv : 0.0f;
@@ -483,11 +483,11 @@ __device__ __forceinline__ void dielectric_f_pdf(float roughness, f3 wo, f3 wi, 
 // ---- Layered "GlossyDiffuse" (dielectric top, Lambert bottom): GlossyDiffuse.h:91-524 ------
 __device__ __forceinline__ float power_heuristic(float fpdf, float gpdf) {  // :91-95 (nf=ng=1)
     float f = 1.0f * fpdf, g = 1.0f * gpdf;
-    return sqr(f) / (sqr(f) + sqr(g));
+    return fdiv(sqr(f), sqr(f) + sqr(g));
 }
 __device__ __forceinline__ float transmittance(float dz, f3 w) {  // :97-105
     if (gabs(dz) <= 1.17549435e-38f) return 1.0f;
-    return pt_expf_neg(-gabs(dz / w.z));  // expf (pt_math.h)
+    return pt_expf_neg(-gabs(fdiv(dz, w.z)));  // expf (pt_math.h)
 }
 __device__ __forceinline__ f3 layer_f(bool top, f3 albedo, float roughness, f3 wo, f3 wi, int mode) {
     if (top) {
@@ -521,7 +521,7 @@ __device__ __forceinline__ bool bs_bad(bool ok, const BSample& b) {
 }
 __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / pdf
     float c = abs_cos_theta(b.dir);
-    return mk(b.color.x * c / b.pdf, b.color.y * c / b.pdf, b.color.z * c / b.pdf);
+    return mk(fdiv(b.color.x * c, b.pdf), fdiv(b.color.y * c, b.pdf), fdiv(b.color.z * c, b.pdf));
 }
 
 __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
@@ -589,7 +589,7 @@ __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness,
             if (depth > 3 && save_max(beta) < 0.25f) {
                 float q = gmax(0.0f, 1.0f - save_max(beta));
                 if (rnd(ns) < q) break;
-                beta = beta / (1.0f - q);
+                beta = beta / (1.0f - q);  // f3 / float: fdiv per channel
             }
             z = (z == thickness) ? 0.0f : thickness;
             beta = beta * tr_w;
@@ -624,7 +624,7 @@ __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness,
                 t1 = t1 * wt;
                 t1 = t1 * tr_wis;
                 t1 = t1 * wis.color;
-                t1 = t1 / wis.pdf;
+                t1 = t1 / wis.pdf;  // f3 / float: fdiv per channel
                 f = f + t1;
             }
             if (itop) {
@@ -662,7 +662,7 @@ __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness,
             }
         }
     }
-    return mk(f.x / 5.0f, f.y / 5.0f, f.z / 5.0f);
+    return mk(fdiv(f.x, 5.0f), fdiv(f.y, 5.0f), fdiv(f.z, 5.0f));
 }
 
 __device__ __noinline__ bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
@@ -690,7 +690,7 @@ __device__ __noinline__ bool layered_sample(uint32_t& seed, f3 albedo, float rou
     float pdf = bs.pdf;
     float z = thickness;
     for (int depth = 0; depth < 10; ++depth) {
-        float rrBeta = save_max(f) / pdf;
+        float rrBeta = fdiv(save_max(f), pdf);
         if (depth > 3 && rrBeta < 0.25f) {
             float q = gmax(0.0f, 1.0f - rrBeta);
             if (rnd(ns) < q) return false;

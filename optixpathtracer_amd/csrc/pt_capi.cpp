@@ -88,8 +88,9 @@ struct EventPool {
 // Device counters: [0] segments [1] nodes visited [2] triangle tests [3] rays [4] stack
 // overflows [5] shadow rays [6] timed trace-kernel rays [7] their bytes [8] strict re-traces
 // [9..13] wave schedule of the trace kernels (pt_stats wave_*) [14] node visits served from LDS
-// [15] items of the timed shading kernel (pt_stats shade_kernel_items).
-constexpr int kCounters = 16;
+// [15] items of the timed shading kernel (pt_stats shade_kernel_items) [16] [17] rays and
+// algorithmic bytes of the k_trace_pair launches alone (pt_stats pair_kernel_*).
+constexpr int kCounters = 18;
 // event pairs held by one renderer before launch_frames retires them (EventPool)
 constexpr size_t kMaxPendingEvents = 4096;
 // the smallest traversal stack of any kernel (pt_device.h stack_capacity: 71 entries for the
@@ -170,6 +171,7 @@ struct pt_renderer {
         RenderKey key;
         hipEvent_t start = nullptr, ready = nullptr;  // recorded on `stream` around the slot's batch
         bool measured = true;                         // its duration is in frame_ms_est
+        bool speculative = false;                     // a cancellable look-ahead batch (cancel_look_ahead)
     };
     RingSlot ring[2];
     int ring_k = 1, ring_last = 0;  // ramp length, slot rendered last
@@ -201,6 +203,11 @@ struct pt_renderer {
     std::vector<hipEvent_t> tev_frame;  // 2 * (max_bounces + 1) events handed to one frame
     double trace_ms = 0.0;
     uint64_t trace_launches = 0;
+    // the k_trace_pair launches among them (fused modes: every timed trace launch after a batch's
+    // k_extend), in a pool of their own so their time is reported per kernel (pt_stats pair_kernel_*)
+    EventPool pev;
+    double pair_ms = 0.0;
+    uint64_t pair_launches = 0;
     // the same for the dominant shading kernel of a bounce (pt_stats shade_kernel_*)
     EventPool sev;
     std::vector<hipEvent_t> sev_frame;
@@ -208,6 +215,15 @@ struct pt_renderer {
     uint64_t shade_launches = 0;
     // render-ahead frames rendered into the ring and calls served from it (pt_stats)
     uint64_t ahead_rendered = 0, ahead_served = 0;
+    // Look-ahead cancellation (cancel_look_ahead, pt_wavefront.hip wf_cancel_poll): the newest
+    // cancel epoch in pinned host memory, which the kernels of a speculative batch read over PCIe
+    // (d_cancel_host) and relay through a device word (d_cancel_seen); cancel_epoch is the epoch
+    // the next speculative batch is enqueued under.
+    unsigned* h_cancel = nullptr;
+    unsigned* d_cancel_host = nullptr;
+    unsigned* d_cancel_seen = nullptr;
+    unsigned cancel_epoch = 0;
+    uint64_t ahead_cancelled = 0;  // look-ahead batches cancelled (pt_stats)
     bool pending = false;
     uint64_t samples = 0;
     double last_ms = 0.0, total_ms = 0.0;
@@ -255,6 +271,13 @@ int collect_pending(pt_renderer* r) {
     size_t n = 0, tn = 0, sn = 0;
     PT_HIP(r->ev.collect(&sum, &n), "frame events");
     PT_HIP(r->tev.collect(&tsum, &tn), "trace-kernel events");
+    double psum = 0.0;
+    size_t pn = 0;
+    PT_HIP(r->pev.collect(&psum, &pn), "pair-kernel events");
+    tsum += psum;  // trace_kernel_* cover k_extend and k_trace_pair together, as before
+    tn += pn;
+    r->pair_ms += psum;
+    r->pair_launches += pn;
     PT_HIP(r->sev.collect(&ssum, &sn), "shading-kernel events");
     r->spec_pending = false;  // ev.collect waited for every enqueued batch
     r->launches += n;
@@ -303,12 +326,13 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
 // are summed at the next pt_synchronize / pt_get_stats / download (collect_pending).
 // frame_stride > 0 (wavefront only): frame first + j is written alone to accum + j * frame_stride.
 int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, double* accum64 = nullptr,
-                  size_t frame_stride = 0) {
+                  size_t frame_stride = 0, bool speculative = false) {
     int rc = PT_OK;
     // callers that never synchronise through the library (pt_stream interop, device sum buffers,
     // loops over pt_launch / pt_display_add_frame) would grow the event pools without bound:
     // past kMaxPendingEvents pairs, retire them first (this waits for the enqueued work)
-    if (r->ev.used + r->tev.used + r->sev.used > kMaxPendingEvents && (rc = collect_pending(r)) != PT_OK) return rc;
+    if (r->ev.used + r->tev.used + r->pev.used + r->sev.used > kMaxPendingEvents && (rc = collect_pending(r)) != PT_OK)
+        return rc;
     const DevScene S = r->scene();
     uint32_t done = 0;
     const uint32_t chunk = (uint32_t)std::max(1, r->frames_per_launch);
@@ -319,6 +343,9 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
     // Dielectric 1239 / 758, Default 255 / 104).
     int kernel = r->kernel;
     if (kernel == PT_KERNEL_AUTO) kernel = PT_KERNEL_WAVEFRONT;
+    // Lambert / Conductor / Dielectric: k_extend at bounce 0, then k_trace_pair per bounce
+    const bool fused = r->material_mode == PT_MAT_LAMBERT || r->material_mode == PT_MAT_CONDUCTOR ||
+                       r->material_mode == PT_MAT_DIELECTRIC;
     if (accum64 && kernel != PT_KERNEL_WAVEFRONT)
         return fail(PT_ERR_INVALID, "fp64 accumulation (pt_set_accum_fp64) runs with the wavefront kernel");
     if (frame_stride && kernel != PT_KERNEL_WAVEFRONT)
@@ -407,8 +434,10 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             const hipEvent_t* sev = nullptr;
             if (r->kernel_timing) {
                 r->tev_frame.resize(2 * (size_t)(r->max_bounces + 1));  // <= max_bounces + 1 trace launches
+                // launch 0 is the batch's k_extend; in the fused modes the others are k_trace_pair
                 for (int k = 0; k <= r->max_bounces; ++k)
-                    PT_HIP(r->tev.next(&r->tev_frame[2 * k], &r->tev_frame[2 * k + 1]), "hipEventCreate");
+                    PT_HIP((k > 0 && fused ? r->pev : r->tev).next(&r->tev_frame[2 * k], &r->tev_frame[2 * k + 1]),
+                           "hipEventCreate");
                 tev = r->tev_frame.data();
                 r->sev_frame.resize(2 * (size_t)(r->max_bounces + 1));  // <= max_bounces shading launches
                 for (int k = 0; k <= r->max_bounces; ++k)
@@ -417,13 +446,24 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
             }
             if (!dual) PT_HIP(hipEventRecord(a, r->stream), "hipEventRecord");
             int n_timed = 0, n_stimed = 0;
-            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, sk ? r->xwf[sk] : r->wf, first + f,
+            WFState wq = sk ? r->xwf[sk] : r->wf;
+            if (speculative && r->d_cancel_seen) {  // a look-ahead batch: its kernels poll the cancel words
+                wq.cancel_host = r->d_cancel_host;
+                wq.cancel_seen = r->d_cancel_seen;
+                wq.cancel_epoch = r->cancel_epoch;
+            }
+            PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, wq, first + f,
                                           nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
                                           // batches add into the sum in frame order; bands touch disjoint pixels
                                           dual && batch > 0 && nband == 1 ? r->ev_accum[(batch - 1) & 1] : nullptr,
                                           dual && nband == 1 ? r->ev_accum[batch & 1] : nullptr, sev, &n_stimed),
                    "wavefront launch");
-            if (tev) r->tev.give_back((size_t)(r->max_bounces + 1 - n_timed));  // pairs never recorded
+            if (tev) {  // pairs never recorded (the last ones handed out)
+                const int unused = r->max_bounces + 1 - n_timed;
+                const int unused_pair = fused ? std::min(unused, r->max_bounces) : 0;
+                r->pev.give_back((size_t)unused_pair);
+                r->tev.give_back((size_t)(unused - unused_pair));
+            }
             if (sev) r->sev.give_back((size_t)(r->max_bounces + 1 - n_stimed));
             if (!dual) PT_HIP(hipEventRecord(b, r->stream), "hipEventRecord");
             if (nband > 1 && band == 0) PT_HIP(hipEventRecord(r->ev_band0, st), "hipEventRecord");
@@ -483,6 +523,7 @@ void ring_free(pt_renderer* r) {
         s.cap = 0;
         s.n = 0;
         s.measured = true;
+        s.speculative = false;
     }
     r->ring_k = 1;
     r->ahead_oom_cap = 1 << 30;
@@ -544,15 +585,43 @@ int ring_reserve(pt_renderer* r, int s, int cap, size_t n3) {
     return PT_OK;
 }
 
+// The cancel words of the look-ahead batches (allocated at the first one; false if they cannot
+// be, and the batch is then enqueued without them).
+bool cancel_words(pt_renderer* r) {
+    if (r->d_cancel_seen) return true;
+    unsigned* h = nullptr;
+    unsigned* d = nullptr;
+    if (hipHostMalloc((void**)&h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    *h = 0;
+    void* hd = nullptr;
+    if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess || hipMalloc((void**)&d, sizeof(unsigned)) != hipSuccess ||
+        hipMemsetAsync(d, 0, sizeof(unsigned), r->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        return false;
+    }
+    r->h_cancel = h;
+    r->d_cancel_host = static_cast<unsigned*>(hd);
+    r->d_cancel_seen = d;
+    r->cancel_epoch = 0;
+    return true;
+}
+
 // Render frames [first, first + n) into ring slot s (room for `cap` frames) as 1-spp images and
-// record its events.
-int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t first, int n, int cap, size_t n3) {
+// record its events.  `speculative`: the look-ahead batch, which cancel_look_ahead can stop.
+int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t first, int n, int cap, size_t n3,
+              bool speculative = false) {
     pt_renderer::RingSlot& sl = r->ring[s];
     sl.n = 0;
     sl.measured = true;
+    sl.speculative = speculative && cancel_words(r);
     int rc = ring_reserve(r, s, std::max(n, cap), n3);
     if (rc == PT_OK) PT_HIP(hipEventRecord(sl.start, r->stream), "hipEventRecord");
-    if (rc == PT_OK) rc = launch_frames(r, sl.d, first, (uint32_t)n, nullptr, n3);
+    if (rc == PT_OK) rc = launch_frames(r, sl.d, first, (uint32_t)n, nullptr, n3, sl.speculative);
     if (rc != PT_OK) return rc;
     PT_HIP(hipEventRecord(sl.ready, r->stream), "hipEventRecord");
     sl.key = k;
@@ -561,6 +630,29 @@ int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t f
     sl.measured = false;
     r->ahead_rendered += (uint64_t)n;
     return PT_OK;
+}
+
+// Cancel the look-ahead batch in flight.  The reference renders one
+// frame per Render() call (OptixRenderer.cpp:617-647) and its viewer moves the camera between
+// calls (OptixView.cpp:133-139); frames pt_render rendered ahead under the old state are then
+// useless, and the next call would wait behind up to ahead_budget_ms of them.  When the state
+// no longer matches the speculative slot (or `force`: the caller is about to change it, and
+// waits on the library stream first), a newer epoch is published in the pinned host word: the
+// batch's kernels see it within about a trace kernel's poll interval and stop
+// (pt_wavefront.hip wf_cancel_poll), the rest of its launches drain as no-ops, and the slot
+// is discarded.  A batch that already finished is kept.
+void cancel_look_ahead(pt_renderer* r, bool force = false) {
+    if (!r->spec_pending || !r->h_cancel) return;
+    pt_renderer::RingSlot& sl = r->ring[r->ring_last];
+    if (sl.n == 0 || !sl.speculative) return;
+    if (!force && sl.key == render_key(r)) return;
+    if (hipEventQuery(sl.ready) == hipSuccess) return;  // done: its frames stay valid for their state
+    (void)hipGetLastError();                            // hipErrorNotReady
+    ++r->cancel_epoch;
+    __atomic_store_n(r->h_cancel, r->cancel_epoch, __ATOMIC_SEQ_CST);
+    sl.n = 0;
+    sl.speculative = false;
+    r->ahead_cancelled++;
 }
 
 // The 1-spp image of frame r->frame_id for pt_render / pt_display_add_frame (OptixRenderer::Render,
@@ -582,6 +674,7 @@ int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nu
     const int kernel = r->kernel == PT_KERNEL_AUTO ? PT_KERNEL_WAVEFRONT : r->kernel;
     const uint32_t f = r->frame_id;
     const bool debug = r->d_debug && r->debug_pixel >= 0;
+    cancel_look_ahead(r);  // a state change since the look-ahead batch: stop it (also with render-ahead now off)
     if (r->render_ahead > 1 && kernel == PT_KERNEL_WAVEFRONT && !debug) {
         ring_measure(r);
         const pt_renderer::RenderKey k = render_key(r);
@@ -621,7 +714,7 @@ int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nu
             // the ramp is done once doubling this slot's length would pass the target length
             if (look_ahead && f == sl.first && sl.n > 1 && 2 * (int)sl.n > kl &&
                 !(r->ring[o].n > 0 && r->ring[o].key == k && r->ring[o].first == next)) {
-                const int lrc = ring_fill(r, o, k, next, kl, ahead_frames(r, n3, false), n3);
+                const int lrc = ring_fill(r, o, k, next, kl, ahead_frames(r, n3, false), n3, true);
                 if (lrc == PT_OK) {
                     r->ring_k = kl;
                     r->ring_last = o;
@@ -992,6 +1085,8 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_display) (void)hipFree(r->d_display);
     if (r->d_counters) (void)hipFree(r->d_counters);
     if (r->d_debug) (void)hipFree(r->d_debug);
+    if (r->d_cancel_seen) (void)hipFree(r->d_cancel_seen);
+    if (r->h_cancel) (void)hipHostFree(r->h_cancel);
     wavefront_free(r->wf);
     for (int k = 1; k < pt_renderer::kMaxWFStreams; ++k) {
         wavefront_free(r->xwf[k]);
@@ -1004,6 +1099,7 @@ int pt_destroy(pt_renderer* r) {
     if (r->dl_stream) (void)hipStreamDestroy(r->dl_stream);
     r->ev.destroy();
     r->tev.destroy();
+    r->pev.destroy();
     r->sev.destroy();
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
@@ -1019,6 +1115,7 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
         if (rc) return rc;
     }
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    cancel_look_ahead(r, true);  // the wait below must not sit behind speculative frames
     PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
     size_t bytes = sizeof(float) * 3 * (size_t)width * (size_t)height;
     if (r->d_frame) (void)hipFree(r->d_frame);
@@ -1059,6 +1156,7 @@ int pt_set_camera(pt_renderer* r, const float position[3], const float inverse_v
     std::memcpy(r->inv_view, inverse_view, sizeof r->inv_view);
     std::memcpy(r->inv_proj, inverse_projection, sizeof r->inv_proj);
     for (pt_renderer* p : r->peers) (void)pt_set_camera(p, position, inverse_view, inverse_projection);
+    cancel_look_ahead(r);  // a moved camera: the look-ahead frames in flight are stale
     return PT_OK;
 }
 
@@ -1069,6 +1167,7 @@ int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count) {
         if (rc) return rc;
     }
     PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    cancel_look_ahead(r, true);  // new lights: the upload below must not wait behind speculative frames
     if (count > r->lights_cap) {
         PT_HIP(hipStreamSynchronize(r->stream), "hipStreamSynchronize");
         if (r->d_lights) (void)hipFree(r->d_lights);
@@ -1102,6 +1201,7 @@ int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces) {
     if (max_bounces < 0) return fail(PT_ERR_INVALID, "pt_set_max_bounces: negative count");
     r->max_bounces = max_bounces;
     for (pt_renderer* p : r->peers) p->max_bounces = max_bounces;
+    cancel_look_ahead(r);
     return PT_OK;
 }
 
@@ -1109,6 +1209,7 @@ int pt_set_material_mode(pt_renderer* r, int32_t mode) {
     if (!r || !valid_mode(mode)) return fail(PT_ERR_INVALID, "pt_set_material_mode: invalid");
     r->material_mode = mode;
     for (pt_renderer* p : r->peers) p->material_mode = mode;
+    cancel_look_ahead(r);
     return PT_OK;
 }
 
@@ -1117,6 +1218,7 @@ int pt_set_kernel(pt_renderer* r, int32_t kernel) {
         return fail(PT_ERR_INVALID, "pt_set_kernel: invalid");
     r->kernel = kernel;
     for (pt_renderer* p : r->peers) p->kernel = kernel;
+    cancel_look_ahead(r);
     return PT_OK;
 }
 
@@ -1387,6 +1489,8 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->triangles = r->ntri;
     out->trace_kernel_ms = r->trace_ms;
     out->trace_kernel_launches = r->trace_launches;
+    out->pair_kernel_ms = r->pair_ms;
+    out->pair_kernel_launches = r->pair_launches;
     out->shadow_rays = c[5];
     out->trace_kernel_rays = c[6];
     out->trace_kernel_bytes = c[7];
@@ -1402,6 +1506,9 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->shade_kernel_items = c[15];
     out->frames_rendered_ahead = r->ahead_rendered;
     out->frames_served_ahead = r->ahead_served;
+    out->look_ahead_cancelled = r->ahead_cancelled;
+    out->pair_kernel_rays = c[16];
+    out->pair_kernel_bytes = c[17];
     // a multi-device renderer reports the work of all its devices (times are device 0's)
     for (pt_renderer* p : r->peers) {
         pt_stats ps;
@@ -1443,9 +1550,12 @@ int pt_stats_reset(pt_renderer* r) {
     r->launches = 0;
     r->trace_ms = 0.0;
     r->trace_launches = 0;
+    r->pair_ms = 0.0;
+    r->pair_launches = 0;
     r->shade_ms = 0.0;
     r->shade_launches = 0;
     r->ahead_rendered = r->ahead_served = 0;
+    r->ahead_cancelled = 0;
     return PT_OK;
 }
 

@@ -70,6 +70,13 @@ struct WFState {
     int* count = nullptr;                   // per bounce: queue, shadow, NEE and sample bucket lengths
     int paths = 0;
     int max_bounces = 0;
+    // Look-ahead cancellation (pt_capi.cpp cancel_look_ahead), set per batch: a speculative
+    // render-ahead batch carries the renderer's cancel words and the epoch it was enqueued under,
+    // and its kernels stop early once the host has published a newer epoch (wf_cancelled,
+    // trace_range).  Null for every other batch: no polling.
+    const unsigned* cancel_host = nullptr;  // pinned host word: the newest cancel epoch (PCIe reads)
+    unsigned* cancel_seen = nullptr;        // device relay of it (agent-scope loads, L2-served)
+    unsigned cancel_epoch = 0;
 };
 size_t wavefront_bytes(int paths, int max_bounces);
 // sum32[i] = (float)sum64[i] (the multi-device fp64 reduce's result -> the fp32 sum buffer)

@@ -12,7 +12,26 @@
 
 #define PT_HD __host__ __device__ __forceinline__
 
+#include "pt_fastdiv.h"
+
+// Correctly rounded division, reciprocal and square root.  On the device they take the shorter
+// exact sequences of pt_fastdiv.h (PT_FAST_DIVSQRT 0 selects the compiler's expansions, for
+// A/B runs); on the host they are the IEEE operations.  Both give the same bits.
+#ifndef PT_FAST_DIVSQRT
+#define PT_FAST_DIVSQRT 1
+#endif
+
 namespace pt {
+
+#if defined(__HIP_DEVICE_COMPILE__) && PT_FAST_DIVSQRT
+PT_HD float fdiv(float a, float b) { return pt_div(a, b); }
+PT_HD float frcp(float x) { return pt_rcp(x); }
+PT_HD float fsqrt(float x) { return pt_sqrt(x); }
+#else
+PT_HD float fdiv(float a, float b) { return a / b; }
+PT_HD float frcp(float x) { return 1.0f / x; }
+PT_HD float fsqrt(float x) { return sqrtf(x); }
+#endif
 
 struct f3 {
     float x, y, z;
@@ -24,7 +43,7 @@ PT_HD f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 PT_HD f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 PT_HD f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 PT_HD f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
-PT_HD f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+PT_HD f3 operator/(f3 a, float s) { return mk(fdiv(a.x, s), fdiv(a.y, s), fdiv(a.z, s)); }
 PT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 PT_HD bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
 
@@ -33,10 +52,10 @@ PT_HD f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
 PT_HD f3 normalize(f3 a) {
-    float i = 1.0f / sqrtf(dot(a, a));
+    float i = frcp(fsqrt(dot(a, a)));
     return a * i;
 }
-PT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
+PT_HD float length(f3 a) { return fsqrt(dot(a, a)); }
 PT_HD float sqr(float x) { return x * x; }
 // glm::max/min/clamp on scalars (func_common.inl:17-30,505-509)
 PT_HD float gmax(float x, float y) { return (x < y) ? y : x; }

@@ -72,6 +72,34 @@ constexpr int kMissTri = -1;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Look-ahead cancellation.  pt_render renders up to 64 frames ahead of
+// the caller on speculation (pt_capi.cpp render_frame_image); when the camera or any other
+// render state changes, those frames are useless and the next call must not wait behind them.
+// The host publishes a new cancel epoch in pinned host memory (cancel_look_ahead); a batch
+// enqueued under an older epoch then stops: every wave of the shading kernels checks at its
+// start and returns, and the trace kernels stop refilling (trace_range), so what is still
+// enqueued of the batch drains in launch gaps.  The host word is read over PCIe by few lanes
+// (`relay`: the first lane of one block in 64, or of one wave per trace workgroup now and
+// then), which raise the device word cancel_seen with an atomic max; everyone else polls that
+// word with agent-scope loads (sc1: L2-served, MI355X_MICROARCH "visibility").  Epochs only
+// grow, so a stale read never cancels a batch enqueued after the cancel.  A cancelled batch's
+// queues stay consistent (every counted entry is written), its ring slot is discarded, and the
+// next batch starts from zeroed counters.
+__device__ __forceinline__ bool wf_cancel_poll(const WFState& W, bool relay) {
+    if (relay) {
+        const unsigned h = __hip_atomic_load(W.cancel_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_max(W.cancel_seen, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned v = __hip_atomic_load(W.cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(v) > W.cancel_epoch;  // wave-uniform
+}
+// Entry check of the shading and setup kernels: the wave returns when its batch is cancelled
+// (a barrier later in the kernel waits only on the surviving waves of the workgroup).
+__device__ __forceinline__ bool wf_cancelled(const WFState& W) {
+    if (!W.cancel_seen) return false;  // not a speculative batch (kernel argument: uniform)
+    return wf_cancel_poll(W, (blockIdx.x & 63) == 0 && threadIdx.x == 0);
+}
+
 // Hit record of a finished extension ray: (path, u, v, tri | back << 31), or a miss.  The
 // shading kernels reconstruct the surface from (tri, u, v) and never read t, so the first word
 // carries the path id and they skip the ray_o read.
@@ -252,6 +280,7 @@ constexpr int kItemBits = 28;  // a queue item index is < 2^28 (kMaxWFPaths); th
 __global__ __launch_bounds__(kBlockWF) void k_camera(WFState W, DevLaunch L, uint32_t frame0, int nf, int lean) {
     const int P = L.width * L.height;
     const int Q = P * nf;
+    if (wf_cancelled(W)) return;  // no barrier below; the queue count stays 0 if wave 0 of block 0 returns
     if (lean) {
         for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P; q += gridDim.x * blockDim.x) {
             f3 o, d;
@@ -328,7 +357,8 @@ struct NoCommit {
 };
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TriBatchLds* tri_lds,
-                                            TravStats& ts, Fetch fetch, Finish finish, Commit commit = Commit{}) {
+                                            TravStats& ts, const WFState& W, Fetch fetch, Finish finish,
+                                            Commit commit = Commit{}) {
     using Tok = decltype(finish(0, *static_cast<const TravState*>(nullptr)));
     constexpr bool kSplit = !std::is_void_v<Tok>;
     using TokS = std::conditional_t<kSplit, Tok, int>;
@@ -341,10 +371,18 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
     // unsigned popcount; ±0.3 %)
     next = __builtin_amdgcn_readfirstlane(next);
     end = __builtin_amdgcn_readfirstlane(end);
+    // look-ahead cancellation (wf_cancel_poll): a cancelled batch's wave stops taking rays from its
+    // slice (it finishes the ones in flight), at the start and at every 16th batch block; one wave
+    // in eight workgroups relays the host word at every 64th
+    uint32_t npoll = 0;
+    if (W.cancel_seen && wf_cancel_poll(W, false)) end = next;
     while (true) {
         // batch block once enough lanes idle (it costs the wave about as much as a step), and
         // at every step once the slice is drained
         if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
+            if (W.cancel_seen && (++npoll & 15) == 0 &&
+                wf_cancel_poll(W, (npoll & 63) == 0 && (blockIdx.x & 7) == 0 && threadIdx.x == 0))
+                end = next;
 #if PT_CYCLE_PROBE
             const uint64_t c0 = probe_clock();
 #else
@@ -425,21 +463,22 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
 // A trace kernel's queue range [first, end): the workgroup's LDS (per-lane stacks, the staged top
 // BVH levels, the triangle batches), then the lane-refilling loop.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
-__device__ __forceinline__ void trace_queue(DevScene S, int first, int end, TravStats& ts, Fetch fetch, Finish finish,
-                                            Commit commit = Commit{}) {
+__device__ __forceinline__ void trace_queue(DevScene S, int first, int end, TravStats& ts, const WFState& W, Fetch fetch,
+                                            Finish finish, Commit commit = Commit{}) {
     __shared__ int stack[kStack * kBlockTrace];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
     __shared__ TriBatchLds tri_batch[kTriBatchWaves];
     stage_top_nodes<kLdsNodes>(S, top);
-    trace_range<ANY, STATS, TEX>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, fetch, finish,
-                                 commit);
+    trace_range<ANY, STATS, TEX>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, W, fetch,
+                                 finish, commit);
 }
 
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
-__device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats& ts, Fetch fetch, Finish finish) {
+__device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats& ts, const WFState& W, Fetch fetch,
+                                            Finish finish) {
     int next, end;
     wave_slice(n, next, end);
-    trace_queue<ANY, STATS, TEX>(S, next, end, ts, fetch, finish);
+    trace_queue<ANY, STATS, TEX>(S, next, end, ts, W, fetch, finish);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -456,7 +495,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_extend(DevScene 
     const float4* rd = W.ray_d[b & 1];
     TravStats ts;
     trace_slice<kRayClosest, STATS, TEX>(
-        S, n_trace, ts,
+        S, n_trace, ts, W,
         [&](int ri, TravState& st) {
             const float4 a = ro[ri], c = rd[ri];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
@@ -525,6 +564,7 @@ __global__ __launch_bounds__(kBlockWF) void k_shadow0_setup(DevScene S, DevLaunc
     const int P1 = L.width * L.height;
     const int nl = L.n_lights;
     const int n = P1 * nl;
+    if (wf_cancelled(W)) return;  // no barrier below
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const int li = k / P1, p = k - li * P1;
         const Hit h = decode_hit(W.hit[p]);  // frame 0's copy (queue 0 is in path order)
@@ -568,7 +608,8 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
     if ((int)(blockIdx.x * kBlock) >= n) return;  // block-uniform
     {
         const int i = (int)(blockIdx.x * kBlock + threadIdx.x);
-        const bool valid = i < n;
+        // a cancelled wave takes no item but still joins the block's appends (block_append)
+        const bool valid = i < n && !wf_cancelled(W);
         bool emit_shadow = false, emit_next = false;
         f3 so, sdir, contrib, o, d, beta;
         uint32_t seed = 0;
@@ -678,7 +719,7 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
         atomicAdd(&L.counters[15], (unsigned long long)P1 * (unsigned long long)nf);
     if ((int)(blockIdx.x * kBlock) >= P1) return;  // block-uniform
     const int p = (int)(blockIdx.x * kBlock + threadIdx.x);
-    const bool valid = p < P1;
+    const bool valid = p < P1 && !wf_cancelled(W);  // a cancelled wave still joins the appends
     int tri = -1;
     SurfaceHit sf;
     if (valid) {
@@ -812,12 +853,14 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
     // per-wave shares of both kinds were slower).
     int first, end;
     wave_slice(n_ext + n_sh, first, end);
-    trace_queue<kRayMixed, STATS, TEX>(S, first, end, ts, fetch, finish, commit);
+    trace_queue<kRayMixed, STATS, TEX>(S, first, end, ts, W, fetch, finish, commit);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
         atomicAdd(&counters[6], (unsigned long long)(n_ext + n_sh));  // rays of timed trace kernels
         atomicAdd(&counters[7], 48ull * (unsigned long long)(n_ext + n_sh));  // their queue bytes
+        atomicAdd(&counters[16], (unsigned long long)(n_ext + n_sh));         // the same, k_trace_pair alone
+        atomicAdd(&counters[17], 48ull * (unsigned long long)(n_ext + n_sh));
     }
     flush_trav_stats<STATS>(counters, ts);
 }
@@ -839,7 +882,7 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
     int nee_bucket = -1, smp_bucket = -1, code = 0;
     f3 so, sdir;
     float stmax = 0.0f;
-    if (i < n) {
+    if (i < n && !wf_cancelled(W)) {  // a cancelled wave still joins the appends
         const float4 hv = W.hit[i];
         const float4 c = rd[i];  // beside the hit record (as k_shade_fused)
         const int path = __float_as_int(hv.x);
@@ -898,7 +941,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(false)) void k_shadow_vis(Dev
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[5], (unsigned long long)n);
     TravStats ts;
     trace_slice<kRayAny, false, TEX>(
-        S, n, ts,
+        S, n, ts, W,
         [&](int j, TravState& st) {
             const float4 a = W.sh_o[j], c = W.sh_d[j];
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
@@ -920,11 +963,12 @@ __global__ __launch_bounds__(kBlockSh) void k_nee_compact(WFState W, int b) {
     if (base >= n) return;  // block-uniform
     __shared__ int lds[kShadeBuckets * (kWavesSh + 1)];
     const int j0 = base + (int)threadIdx.x * kCompactPer;
+    const bool cx = wf_cancelled(W);  // a cancelled wave compacts nothing but joins the barriers
     int v[kCompactPer];
     int c[kShadeBuckets] = {};
 #pragma unroll
     for (int k = 0; k < kCompactPer; ++k) {
-        v[k] = j0 + k < n ? W.vis[j0 + k] : -1;
+        v[k] = j0 + k < n && !cx ? W.vis[j0 + k] : -1;
 #pragma unroll
         for (int q = 0; q < kShadeBuckets; ++q) c[q] += (v[k] >= 0 && (v[k] >> kItemBits) == q) ? 1 : 0;
     }
@@ -996,8 +1040,9 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene 
     if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters)
         atomicAdd(&L.counters[15], (unsigned long long)bucket_total(W, b, kNee0));
     if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kNee0)) return;  // block-uniform
+    if (wf_cancelled(W)) return;  // no barrier below
     const int j = bucket_entry(W, W.nq, b, kNee0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
-    if (j < 0) return;  // no barrier below
+    if (j < 0) return;
     const float4 hv = W.hit[j], c = W.ray_d[b & 1][j];
     const int path = __float_as_int(hv.x);
     const Hit h = decode_hit(hv);
@@ -1036,7 +1081,7 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_smp(DevScene 
     bool emit_next = false;
     f3 o, d;
     int path = 0;
-    if (j >= 0) {
+    if (j >= 0 && !wf_cancelled(W)) {  // a cancelled wave still joins the appends
         const float4 hv = W.hit[j], c = W.ray_d[b & 1][j];
         path = __float_as_int(hv.x);
         const Hit h = decode_hit(hv);

@@ -1,10 +1,13 @@
 #!/bin/bash
-# Round evidence on the GPU box (repo root), in two gpurun calls (each under gpurun's limit):
-#   tools/round.sh TAG bench    GPU tests, then bench.py on every BASELINE config
+# Round evidence on the GPU box (repo root), in two gpurun calls (each under gpurun's limit),
+# profile FIRST, so the bench lines read PMC figures of their own sources:
 #   tools/round.sh TAG profile  tools/profile.sh (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE
-#                               passes) on the headline, then the SQ/TCC/TCP passes of tools/pmc.sh
-#                               for profiles/valu.json and the TA/TD passes of tools/pmc_ta.sh for
-#                               profiles/vmem.json
+#                               passes) on the headline, the SQ/TCC/TCP passes of tools/pmc.sh
+#                               for profiles/valu.json, the TA/TD passes of tools/pmc_ta.sh for
+#                               profiles/vmem.json, the k_shade_nee VALU passes and kernel stats of
+#                               configs 3 and 5; then, here: tools/store_round.py TAG profile
+#   tools/round.sh TAG bench    GPU tests, then bench.py on every BASELINE config; then, here:
+#                               tools/store_round.py TAG bench
 # Every step has its own time limit and the chain stops at the first failure.
 set -e
 TAG=${1:-r03}
@@ -41,5 +44,12 @@ else
       > "$OUT/shv_$cfg.log" 2>&1
     python3 tools/pmc_summary.py "$OUT/shv_$cfg" k_shade_nee --shade-json "$OUT/shade_valu_config$cfg.json" \
       --source "tools/round.sh $TAG profile (rocprofv3 SQ pass, perf_probe --scene $sc --fpl 64 --spp 64)" | tail -3
+  done
+  # kernel stats of the Default-mode configs' own bench command
+  for cfg in 3 5; do
+    echo "[round] kernel trace, config $cfg"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_config$cfg" -o run -- \
+      python3 bench.py --config $cfg --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --reference-loops 0 \
+      > "$OUT/kt_config$cfg.json" 2> "$OUT/kt_config$cfg.log"
   done
 fi

@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Copy a tools/round.sh TAG run from gpurun_out/ into profiles/ and refresh the derived files.
 
-    python tools/store_round.py TAG
-Copies the bench JSONs of every config, the GPU-test log, the rocprofv3 kernel stats (two-stream
-and one-stream passes) and the PMC traces; writes profiles/traffic.json and profiles/shade_pmc.json
-(tools/shade_pmc.py over the one-stream kernel stats).
+    python tools/store_round.py TAG profile   after `tools/round.sh TAG profile` (run first)
+    python tools/store_round.py TAG bench     after `tools/round.sh TAG bench`
+profile: the rocprofv3 kernel stats (two-stream and one-stream passes, and configs 3 and 5) and
+the PMC traces; writes profiles/traffic.json, profiles/shade_pmc.json (tools/shade_pmc.py over
+the one-stream kernel stats), valu.json, vmem.json and shade_valu_config*.json, which the bench
+lines then report as figures of their own sources.  bench: the bench JSONs of every config and
+the GPU-test log.
 """
 import shutil
 import subprocess
@@ -16,15 +19,22 @@ ROOT = Path(__file__).resolve().parent.parent
 
 def main():
     tag = sys.argv[1]
+    part = sys.argv[2] if len(sys.argv) > 2 else "profile"
     prof, rnd, out = ROOT / "gpurun_out" / f"prof_{tag}", ROOT / "gpurun_out" / f"round_{tag}", ROOT / "profiles"
+    if part == "bench":
+        cp = [(rnd / "gputest.log", f"{tag}_gputest.log")]
+        cp += [(rnd / f"bench_config{c}.json", f"{tag}_bench_config{c}.json") for c in ("2", "3", "4l", "5", "4d")]
+        for src, dst in cp:
+            shutil.copyfile(src, out / dst)
+        return
     cp = [(prof / "kt" / "run_kernel_stats.csv", f"{tag}_wavefront_kernel_stats.csv"),
           (prof / "kt1" / "run_kernel_stats.csv", f"{tag}_wavefront_kernel_stats_single_stream.csv"),
           (prof / "fetch" / "run_counter_collection.csv", f"{tag}_wavefront_pmc_fetch_trace.csv"),
           (prof / "write" / "run_counter_collection.csv", f"{tag}_wavefront_pmc_write_trace.csv"),
           (prof / "traffic.json", f"{tag}_wavefront_traffic.json"),
-          (prof / "traffic.json", "traffic.json"),
-          (rnd / "gputest.log", f"{tag}_gputest.log")]
-    cp += [(rnd / f"bench_config{c}.json", f"{tag}_bench_config{c}.json") for c in ("2", "3", "4l", "5", "4d")]
+          (prof / "traffic.json", "traffic.json")]
+    cp += [(rnd / f"kt_config{c}" / "run_kernel_stats.csv", f"{tag}_kernel_stats_config{c}.csv") for c in ("3", "5")
+           if (rnd / f"kt_config{c}" / "run_kernel_stats.csv").exists()]
     for src, dst in cp:
         shutil.copyfile(src, out / dst)
     pmc = subprocess.run([sys.executable, str(ROOT / "tools" / "shade_pmc.py"),

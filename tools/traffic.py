@@ -25,8 +25,9 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from optixpathtracer_amd.provenance import kernel_sources_sha  # noqa: E402
 
-# dominant kernels: the megakernel, or the wavefront's trace kernels taken as one group
-GROUPS = {"k_render_mega": ("k_render_mega",), "k_extend+k_trace_pair": ("k_extend", "k_trace_pair")}
+# dominant kernels, per kernel: the megakernel, the fused modes'
+# k_trace_pair, the Default / Layered modes' k_shade_nee
+GROUPS = {"k_render_mega": ("k_render_mega",), "k_trace_pair": ("k_trace_pair",), "k_shade_nee": ("k_shade_nee",)}
 
 
 def timed_instance(name: str) -> bool:
