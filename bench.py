@@ -18,16 +18,19 @@ more step with 1024 frames per rank reports the weak-scaling rate as `value_weak
 spp per step); the driver's default run is configs[1].
 
 Extra fields: `roofline` (HBM roofline of the mode's dominant kernel, measured with one HIP event
-pair per launch on the stream it runs on: in the Lambert / Conductor / Dielectric modes the
-wavefront's trace kernels k_extend + k_trace_pair, 48 algorithmic bytes per traced ray, ray read +
-result write, with `vmem` -- the same launches against the CU vector-memory path that binds them,
-16-B lane loads from global memory per second against one line per CU-cycle; in the Default /
-Layered modes k_shade_nee, the layered NEE eval, 216 algorithmic bytes per item, with `valu` -- its
-VALU issue fraction from a committed PMC summary; `pipeline_gbps` is SURVEY.md §8(d)'s whole-path
-396 B/segment + 12 B/sample over the render time; `traffic` is the PMC HBM bytes per launch from
-profiles/traffic.json), `cpu_baseline` (the CPU oracle, oracle/, timed on a bounded band of the
-same workload on the host cores, rank 0 at N=1 only) and `distributed` (the process group's
-backend and rank count and the reduce time per step).
+pair per launch on the stream it runs on, per kernel: in the Lambert / Conductor / Dielectric modes
+k_trace_pair (the shadow rays of bounce b and the extension rays of b+1 of a 64-frame batch), 48
+algorithmic bytes per traced ray, ray read + result write; in the Default / Layered modes
+k_shade_nee, the layered NEE eval, 216 algorithmic bytes per item.  `window` says the timed
+region's launch windows are concurrent with the other wavefront stream's kernels (`single_stream`
+repeats the kernel alone); `binding` names the unit the PMC counters show binds the kernel -- the
+vector memory path for k_trace_pair (`vmem`: 16-B lane loads per second against one line per
+CU-cycle, with TA/TD busy from a committed PMC summary), VALU issue x lane utilisation for
+k_shade_nee (`valu`); `pipeline_gbps` is SURVEY.md §8(d)'s whole-path 396 B/segment + 12 B/sample
+over the render time; `traffic` is the PMC HBM bytes per launch from profiles/traffic.json),
+`cpu_baseline` (the CPU oracle, oracle/, timed on a bounded band of the same workload on the host
+cores, rank 0 at N=1 only) and `distributed` (the process group's backend and rank count and the
+reduce time per step).
 """
 from __future__ import annotations
 
@@ -507,9 +510,9 @@ def main():
                 "frames_per_launch": args.frames_per_launch,
                 "parallelism": f"spp-shard x{world}",
                 "lbvh_build_ms": round(bvh_ms, 3),
-                # pt_options.bvh_builder = PT_BVH_AUTO: the host binned-SAH binary tree (<= 4 M
-                # triangles) collapsed to BVH4 on the GPU; the time above covers both
-                "bvh_builder": "auto (host binned SAH + GPU SAH-optimal BVH4 collapse)",
+                # pt_options.bvh_builder = PT_BVH_AUTO: the binned-SAH binary tree built on the GPU
+                # (pt_sah_gpu.hip) and collapsed to BVH4 on the GPU; the time above covers both
+                "bvh_builder": "auto (GPU binned SAH + GPU SAH-optimal BVH4 collapse)",
                 "primary_dedup": args.kernel != 0,
             },
             # one extra step with pt_set_primary_dedup(0): each frame traces its own copy of the
@@ -592,13 +595,15 @@ def main():
 
             fid = r.frame_id
             e4 = ref_loop(args.reference_loops)
-            # Latency of a state change in the steady state: after 200 sequential
-            # calls (a look-ahead batch in flight), the camera moves and one call is timed: it waits
-            # for the batch already enqueued (bounded by pt_set_render_ahead_budget), then renders
-            # and downloads its own frame.  Median of 3.
+            # Latency of a state change in the steady state:
+            # after 200 sequential calls (a look-ahead batch in flight), the camera moves and one call
+            # is timed.  pt_set_camera cancels the speculative batch (pt_capi.cpp cancel_look_ahead:
+            # its kernels stop at their next poll), so the call waits for little more than its own
+            # frame's render and download.  Median of 3.
             import statistics
 
             lat = []
+            canc0 = r.stats()["look_ahead_cancelled"]
             for k in range(3):
                 r.SetCameraBlender(scene.camera_blender_pos, scene.camera_blender_rot, scene.fov_deg)
                 r.frame_id = 0
@@ -611,6 +616,7 @@ def main():
                 lat.append(time.perf_counter() - t)
             r.SetCameraBlender(scene.camera_blender_pos, scene.camera_blender_rot, scene.fov_deg)
             r.synchronize()
+            n_cancelled = r.stats()["look_ahead_cancelled"] - canc0
             r.set_render_ahead(1)
             n_off = min(args.reference_loops, 64)
             e5 = ref_loop(n_off)
@@ -622,6 +628,7 @@ def main():
                                              "frame per call (the reference's DrawOptix loop), render-ahead on, "
                                              "kernel timing off",
                                      "first_call_after_change_ms": round(1e3 * statistics.median(lat), 3),
+                                     "look_ahead_cancelled": n_cancelled,
                                      "render_ahead_budget_ms": 50.0,
                                      # one frame per call: two row bands on the two streams (pt_set_band_split)
                                      "no_render_ahead": {"calls": n_off, "ms_per_call": round(e5 / n_off * 1e3, 3),

@@ -35,13 +35,17 @@ extern "C" {
 /* Render-kernel variants (all produce the same image). */
 #define PT_KERNEL_MEGA 0      /* one thread per pixel, frames looped in registers */
 #define PT_KERNEL_WAVEFRONT 1 /* wavefront: per-bounce kernels over SoA ray/hit queues, wave compaction */
-#define PT_BVH_AUTO 0          /* default: PT_BVH_SAH up to 4 M triangles, PT_BVH_PLOC beyond */
+#define PT_BVH_AUTO 0          /* default: PT_BVH_SAH_GPU */
 #define PT_BVH_LBVH 1          /* GPU Karras LBVH -> BVH4 (fastest build) */
 #define PT_BVH_SAH 2           /* host binned-SAH binary tree -> the GPU SAH-optimal BVH4 collapse: 13 %
                                   fewer node visits per ray than PLOC; 19 ms at 35k,
-                                  115 ms at 250k triangles */
+                                  115 ms at 250k triangles on one host thread.  The reference build of
+                                  PT_BVH_SAH_GPU's tree. */
 #define PT_BVH_PLOC 3          /* GPU PLOC clustering -> the same collapse (fast build, near-SAH)
                                   -- every builder gives the same images bit for bit */
+#define PT_BVH_SAH_GPU 4       /* PT_BVH_SAH's tree built on the GPU (pt_sah_gpu.hip): the same BVH4 bit
+                                  for bit.  Changelog: round 4 made 0 = AUTO (PLOC moved 0 -> 3);
+                                  round 5 added this value and made it AUTO's choice. */
 
 #define PT_KERNEL_AUTO 2      /* the faster path (measured): currently the wavefront in every mode */
 
@@ -120,7 +124,10 @@ typedef struct pt_stats {
     uint64_t rays;
     uint64_t stack_overflows;
     /* trace kernels of the wavefront path (k_extend, and k_trace_pair in the fused modes), only
-       timed while pt_set_kernel_timing(r, 1): summed per-launch HIP-event time and launch count */
+       timed while pt_set_kernel_timing(r, 1): summed per-launch HIP-event time and launch count.
+       A one-frame call in row bands (pt_set_band_split) times each band's launches separately,
+       and the two bands run at the same time, so its per-launch times are per band and overlap
+       (not comparable with a multi-frame call's). */
     double trace_kernel_ms;
     uint64_t trace_kernel_launches;
     uint64_t shadow_rays;        /* NEE shadow rays traced since pt_stats_reset */

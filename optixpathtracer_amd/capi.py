@@ -15,7 +15,7 @@ LIB_PATH = _HERE / "libptamd.so"
 
 PT_MAT_DEFAULT, PT_MAT_LAMBERT, PT_MAT_CONDUCTOR, PT_MAT_DIELECTRIC, PT_MAT_LAYERED = range(5)
 PT_KERNEL_MEGA, PT_KERNEL_WAVEFRONT, PT_KERNEL_AUTO = 0, 1, 2
-PT_BVH_AUTO, PT_BVH_LBVH, PT_BVH_SAH, PT_BVH_PLOC = 0, 1, 2, 3
+PT_BVH_AUTO, PT_BVH_LBVH, PT_BVH_SAH, PT_BVH_PLOC, PT_BVH_SAH_GPU = 0, 1, 2, 3, 4
 PT_OK, PT_ERR_INVALID, PT_ERR_HIP, PT_ERR_STATE, PT_ERR_NOMEM = 0, -1, -2, -3, -4
 
 MATERIAL_MODES = {

@@ -689,13 +689,14 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
     temp_bytes = std::max(temp_bytes, scan_bytes);
     PT_TRY(hipMalloc(&temp, temp_bytes > 0 ? temp_bytes : 16));
     PT_TRY(hipEventRecord(e0, stream));
-    if (in.builder == kBuilderSAH && n > 1) {
+    if ((in.builder == kBuilderSAH || in.builder == kBuilderSAHGPU) && n > 1) {
         // host binned-SAH binary tree, then the same leaf gather and SAH-optimal collapse
         std::vector<uint32_t> order;
         std::vector<int2> hchild, hrange;
         std::vector<float4> hbox;
-        sah_binary_tree(in.tri_host, n, order, hchild, hrange, hbox);
-        if (PT_SAH_REINSERT > 0) {
+        const bool on_gpu = in.builder == kBuilderSAHGPU;
+        if (!on_gpu) sah_binary_tree(in.tri_host, n, order, hchild, hrange, hbox);
+        if (!on_gpu && PT_SAH_REINSERT > 0) {
             // kept only when it cuts the binary tree's cost by 2 % or more: Sponza-class 8.9 % ->
             // +0.5 % Msamples/s; the sphere box 0.13 % -> one level deeper and -1.1 to -1.6 %
             // (profiles/r04u_ab_reinsert_sponza.log)
@@ -721,10 +722,14 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
             PT_TRY(hipMalloc(pr.first, pr.second));
             owned.push_back(*pr.first);
         }
-        PT_TRY(hipMemcpyAsync(dfs, order.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice, stream));
-        PT_TRY(hipMemcpyAsync(schild, hchild.data(), sizeof(int2) * (size_t)nbin, hipMemcpyHostToDevice, stream));
-        PT_TRY(hipMemcpyAsync(srange, hrange.data(), sizeof(int2) * (size_t)nbin, hipMemcpyHostToDevice, stream));
-        PT_TRY(hipMemcpyAsync(sbox, hbox.data(), sizeof(float4) * 2 * (size_t)nbin, hipMemcpyHostToDevice, stream));
+        if (on_gpu) {
+            PT_TRY(sah_build_gpu(in.tri_orig, n, dfs, schild, srange, sbox, stream));
+        } else {
+            PT_TRY(hipMemcpyAsync(dfs, order.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice, stream));
+            PT_TRY(hipMemcpyAsync(schild, hchild.data(), sizeof(int2) * (size_t)nbin, hipMemcpyHostToDevice, stream));
+            PT_TRY(hipMemcpyAsync(srange, hrange.data(), sizeof(int2) * (size_t)nbin, hipMemcpyHostToDevice, stream));
+            PT_TRY(hipMemcpyAsync(sbox, hbox.data(), sizeof(float4) * 2 * (size_t)nbin, hipMemcpyHostToDevice, stream));
+        }
         hipLaunchKernelGGL(k_gather, dim3(grid_for(n, 256)), dim3(256), 0, stream, in.tri_orig, in.nrm_orig,
                            in.uv_orig, dfs, n, out.isect, out.shade, out.tuv, sleaf, spleaf);
         PT_TRY(hipGetLastError());
@@ -736,7 +741,7 @@ hipError_t lbvh_build(const BuildInput& in, BuildOutput& out, hipStream_t stream
         B.pleaf = spleaf;
         root = 0;
     }
-    if (in.builder != kBuilderSAH || n <= 1) {
+    if ((in.builder != kBuilderSAH && in.builder != kBuilderSAHGPU) || n <= 1) {
         float3 cmin = make_float3(in.cmin[0], in.cmin[1], in.cmin[2]);
         float ex = in.cmax[0] - in.cmin[0], ey = in.cmax[1] - in.cmin[1], ez = in.cmax[2] - in.cmin[2];
         float3 cinv = make_float3(ex > 0.0f ? 1.0f / ex : 0.0f, ey > 0.0f ? 1.0f / ey : 0.0f,

@@ -710,10 +710,12 @@ int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nu
             r->ahead_served++;
             const int o = s ^ 1;
             const uint32_t next = sl.first + sl.n;
-            const int kl = ahead_frames(r, n3, true);  // the full ramp length now
-            // the ramp is done once doubling this slot's length would pass the target length
-            if (look_ahead && f == sl.first && sl.n > 1 && 2 * (int)sl.n > kl &&
-                !(r->ring[o].n > 0 && r->ring[o].key == k && r->ring[o].first == next)) {
+            // the ramp is done once doubling this slot's length would pass the target length (the
+            // length, a device-memory query, only for a call that may enqueue: ADVICE round 4)
+            const bool may_look = look_ahead && f == sl.first && sl.n > 1 &&
+                                  !(r->ring[o].n > 0 && r->ring[o].key == k && r->ring[o].first == next);
+            const int kl = may_look ? ahead_frames(r, n3, true) : 0;  // the full ramp length now
+            if (may_look && 2 * (int)sl.n > kl) {
                 const int lrc = ring_fill(r, o, k, next, kl, ahead_frames(r, n3, false), n3, true);
                 if (lrc == PT_OK) {
                     r->ring_k = kl;
@@ -824,7 +826,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     if (!devlist.empty()) opt.device = devlist[0];
     if (!valid_mode(opt.material_mode)) return fail(PT_ERR_INVALID, "pt_create: invalid material_mode");
     if (opt.bvh_builder != PT_BVH_AUTO && opt.bvh_builder != PT_BVH_PLOC && opt.bvh_builder != PT_BVH_LBVH &&
-        opt.bvh_builder != PT_BVH_SAH)
+        opt.bvh_builder != PT_BVH_SAH && opt.bvh_builder != PT_BVH_SAH_GPU)
         return fail(PT_ERR_INVALID, "pt_create: invalid bvh_builder");
     if (opt.kernel != PT_KERNEL_MEGA && opt.kernel != PT_KERNEL_WAVEFRONT && opt.kernel != PT_KERNEL_AUTO)
         return fail(PT_ERR_INVALID, "pt_create: invalid kernel");
@@ -950,6 +952,14 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         if (e__ != hipSuccess) return cleanup_fail(hip_fail(e__, where)); \
     } while (0)
     PT_HIPC(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking), "hipStreamCreate");
+    // The download stream and the second wavefront stream right after the library stream: HIP
+    // spreads streams over GPU_MAX_HW_QUEUES (4) hardware queues in creation order, and two streams
+    // that land on one queue run in sequence.  Created lazily (first pt_render, first two-batch
+    // render) they could share a queue with r->stream after other streams had been created in
+    // between; then a pt_render download waited for the look-ahead batch behind it on that queue.
+    PT_HIPC(hipStreamCreateWithFlags(&r->dl_stream, hipStreamNonBlocking), "hipStreamCreate");
+    PT_HIPC(hipStreamCreateWithFlags(&r->xstream[1], hipStreamNonBlocking), "hipStreamCreate");
+    PT_HIPC(hipEventCreateWithFlags(&r->ev_join[1], hipEventDisableTiming), "hipEventCreate");
     PT_HIPC(hipMalloc(&r->d_counters, kCounters * sizeof(unsigned long long)), "hipMalloc counters");
     PT_HIPC(hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream), "hipMemset");
     PT_HIPC(hipMalloc(&r->d_mats, sizeof(float4) * mats.size()), "hipMalloc mats");
@@ -991,14 +1001,12 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
         in.nrm_orig = d_nrm_orig;
         in.uv_orig = d_uv_orig;
         in.n = (int)ntri;
-        // AUTO: the host SAH tree (fewest node visits) up to 4 M triangles (≈ 0.1 s per 250 k on one
-        // host thread), the GPU PLOC tree beyond
-        constexpr size_t kAutoSahMaxTris = size_t(1) << 22;
+        // AUTO: the binned-SAH tree (fewest node visits of the builders), built on the
+        // GPU; every peer of a multi-device renderer builds its own on its own device
         in.builder = opt.bvh_builder == PT_BVH_LBVH   ? kBuilderLBVH
                      : opt.bvh_builder == PT_BVH_PLOC ? kBuilderPLOC
                      : opt.bvh_builder == PT_BVH_SAH  ? kBuilderSAH
-                     : ntri <= kAutoSahMaxTris        ? kBuilderSAH
-                                                      : kBuilderPLOC;
+                                                      : kBuilderSAHGPU;
         in.tri_host = tri.data();
         for (int a = 0; a < 3; ++a) {
             in.cmin[a] = cmin[a];

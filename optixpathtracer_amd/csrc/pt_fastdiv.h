@@ -9,17 +9,22 @@
 // Division and square root are 27 % of the layered NEE kernel's VALU instructions (DESIGN §5,
 // round-4 census).  The sequences here are shorter and exact:
 //
-// * div_short: the compiler's sequence minus its second residual correction (9 instructions).
-//   After v_div_scale the scaled denominator d has 1/d normal, and v_rcp + one Newton step gives
-//   y = RN(1/d) exactly there (tools/rcp_exhaustive.hip, all 2^32 inputs).  With y = RN(1/d)
-//   and q0 = RN(n*y) within an ulp of n/d, the remainder r = n - d*q0 is exact and
-//   RN(q0 + r*y) = RN(n/d) (Markstein's theorem); v_div_fmas / v_div_fixup still apply the
-//   hardware's scaling and special cases.  Proof run: tools/divsqrt_exhaustive.hip.
-// * rcp_fast / pt_rcp: v_rcp + one Newton step (3 instructions), exact wherever the result is a
-//   normal float and x is (all 2^32 inputs checked); the rest take the IEEE division.
-// * sqrt_fast / pt_sqrt: v_sqrt and the +-1 ulp residual correction without the scaling and the
-//   class fix-up, exact for every x >= 2^-96 (all 2^32 inputs checked); smaller x take sqrtf.
-// The fallbacks are divergent branches that a wave skips when none of its lanes needs them.
+// * div_short / pt_div: the compiler's sequence minus its second residual correction (9
+//   instructions).  After v_div_scale the scaled denominator d has 1/d normal, and v_rcp + one
+//   Newton step gives y = RN(1/d) exactly there (tools/rcp_exhaustive.hip, all 2^32 inputs).
+//   With y = RN(1/d) and q0 = RN(n*y) within an ulp of n/d, the remainder r = n - d*q0 is exact
+//   and RN(q0 + r*y) = RN(n/d) (Markstein's theorem); v_div_fixup still applies the special
+//   cases.  When v_div_scale flags a result v_div_fmas must rescale (a denormal or near-overflow
+//   quotient) the lane takes the compiler's last step in a branch that waves skip.
+// * sqrt_fast / pt_sqrt_nb: v_sqrt and the +-1 ulp residual correction with the compiler's input
+//   scaling below 2^-96, without its zero / infinity class fix-up: 14 instructions, branchless.
+// * rcp_fast / pt_rcp, pt_sqrt: guarded fast paths with an IEEE fallback branch; exact, but
+//   measured slower in the kernels (register pressure) and not the defaults.
+// Proofs: tools/divsqrt_exhaustive.hip -- every fp32 input for the reciprocal and both square
+// roots; for the division every pair of significands (2^46) in 16 exponent regimes covering
+// each v_div_scale case, plus 9 * 2^34 random pairs with specials; 0 mismatches
+// (profiles/r05_dsx_*.log).
+
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,11 +42,9 @@ __device__ __forceinline__ float div_short(float a, float b) {
     // v_div_scale flags a quotient that v_div_fmas must rescale (near overflow, or a denormal
     // result, whose coarser rounding grid the one-correction quotient does not respect: one
     // mismatch in 2^34 random pairs without this).  Those lanes take the compiler's last step.
-    // (The empty asm keeps the branch: if-converted, both steps would run on every lane.)
-    if (scale) {
-        asm volatile("");
-        q = __builtin_amdgcn_div_fmasf(__builtin_fmaf(-d, q, n), y, q, true);
-    }
+    // (Expected false, so the compiler keeps it a branch instead of computing both steps on
+    // every lane; no asm barrier, which would also stop it from merging equal divisions.)
+    if (__builtin_expect(scale, 0)) q = __builtin_amdgcn_div_fmasf(__builtin_fmaf(-d, q, n), y, q, true);
     return __builtin_amdgcn_div_fixupf(q, b, a);
 }
 
@@ -83,6 +86,17 @@ __device__ __forceinline__ float pt_sqrt(float x) {
         y = __builtin_sqrtf(x);
     }
     return y;
+}
+
+// Branchless square root: the compiler's input scaling below 2^-96 (x * 2^32, result * 2^-16)
+// around sqrt_fast's correction, without its zero / infinity class fix-up (sqrt_fast returns +-0
+// and +inf unchanged; all 2^32 inputs checked).
+__device__ __forceinline__ float pt_sqrt_nb(float x) {
+    const bool tiny = x < 0x1.0p-96f;
+    const float xs = tiny ? x * 0x1.0p+32f : x;
+    float y;
+    (void)sqrt_fast(xs, y);
+    return tiny ? y * 0x1.0p-16f : y;
 }
 
 }  // namespace pt

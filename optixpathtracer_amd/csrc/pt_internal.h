@@ -22,16 +22,24 @@ struct BuildInput {
 };
 constexpr int kBuilderPLOC = 0;
 constexpr int kBuilderLBVH = 1;
-constexpr int kBuilderSAH = 2;
+constexpr int kBuilderSAH = 2;     // host binned SAH (pt_sah.cpp)
+constexpr int kBuilderSAHGPU = 3;  // the same tree built on the GPU (pt_sah_gpu.hip)
 
 // Host binned-SAH binary tree (pt_sah.cpp) in the GPU builders' layout: order = original triangle
 // per DFS leaf, child codes (>= 0 internal, ~k DFS leaf k), leaf ranges and plain boxes; root 0.
 void sah_binary_tree(const float4* tri, int n, std::vector<uint32_t>& order, std::vector<int2>& child,
                      std::vector<int2>& range, std::vector<float4>& box);
+// The same binary tree built on the GPU (pt_sah_gpu.hip): order, child, range and box are device
+// arrays of n, n - 1, n - 1 and 2 (n - 1) entries; identical to sah_binary_tree's up to the
+// internal node numbering (root 0).  Synchronises `stream`.
+hipError_t sah_build_gpu(const float4* tri, int n, uint32_t* order, int2* child, int2* range, float4* box,
+                         hipStream_t stream);
 // Insertion-based optimisation of that tree in place (pt_sah.cpp); returns the relative cost cut.
-// PT_SAH_REINSERT = the most rounds kBuilderSAH runs (0: off).
+// PT_SAH_REINSERT = the most rounds kBuilderSAH runs (0: off, the default since round 5: it measured
+// 0.0 % on Sponza-class for 30-55 ms of host build, profiles/r04v_ab_reinsert_undo_sponza.log, and
+// the GPU builder reproduces the unrefined tree).
 #ifndef PT_SAH_REINSERT
-#define PT_SAH_REINSERT 16
+#define PT_SAH_REINSERT 0
 #endif
 double sah_reinsert(std::vector<uint32_t>& order, std::vector<int2>& child, std::vector<int2>& range,
                     std::vector<float4>& box, const float4* tri, int rounds);

@@ -14,19 +14,32 @@
 
 #include "pt_fastdiv.h"
 
-// Correctly rounded division, reciprocal and square root.  On the device they take the shorter
-// exact sequences of pt_fastdiv.h (PT_FAST_DIVSQRT 0 selects the compiler's expansions, for
-// A/B runs); on the host they are the IEEE operations.  Both give the same bits.
+// Correctly rounded division, reciprocal and square root.  On the device the division and the
+// square root take the shorter exact sequences of pt_fastdiv.h; on the host they are the IEEE
+// operations.  Both give the same bits.  Measured per operation (interleaved A/B, DESIGN.md §5,
+// profiles/r05d_ab_*.log): PT_FAST_DIV 1 and PT_FAST_SQRT 2 (branchless) took the Default /
+// Layered / Sponza-class configs +9.8 / +11.6 / +6.7 % with Dielectric unchanged; the guarded
+// reciprocal (PT_FAST_RCP 1) raised the Conductor kernels' registers 80 -> 108 VGPRs and lost,
+// so 1 / x stays the compiler's.  PT_FAST_DIVSQRT 0 selects the compiler's expansions throughout.
 #ifndef PT_FAST_DIVSQRT
 #define PT_FAST_DIVSQRT 1
+#endif
+#ifndef PT_FAST_DIV
+#define PT_FAST_DIV PT_FAST_DIVSQRT
+#endif
+#ifndef PT_FAST_RCP
+#define PT_FAST_RCP 0
+#endif
+#ifndef PT_FAST_SQRT
+#define PT_FAST_SQRT (PT_FAST_DIVSQRT ? 2 : 0)
 #endif
 
 namespace pt {
 
-#if defined(__HIP_DEVICE_COMPILE__) && PT_FAST_DIVSQRT
-PT_HD float fdiv(float a, float b) { return pt_div(a, b); }
-PT_HD float frcp(float x) { return pt_rcp(x); }
-PT_HD float fsqrt(float x) { return pt_sqrt(x); }
+#if defined(__HIP_DEVICE_COMPILE__)
+PT_HD float fdiv(float a, float b) { return PT_FAST_DIV ? pt_div(a, b) : a / b; }
+PT_HD float frcp(float x) { return PT_FAST_RCP == 1 ? pt_rcp(x) : PT_FAST_RCP == 2 ? pt_div(1.0f, x) : 1.0f / x; }
+PT_HD float fsqrt(float x) { return PT_FAST_SQRT == 1 ? pt_sqrt(x) : PT_FAST_SQRT == 2 ? pt_sqrt_nb(x) : sqrtf(x); }
 #else
 PT_HD float fdiv(float a, float b) { return a / b; }
 PT_HD float frcp(float x) { return 1.0f / x; }

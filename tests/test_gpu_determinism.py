@@ -49,7 +49,7 @@ def _compare(r, o, rays):
     return hit.mean()
 
 
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_round1_event_ray(sponza, builder):
     from optixpathtracer_amd.renderer import setup_renderer
     from oracle.oracle import OracleScene
@@ -64,7 +64,7 @@ def test_round1_event_ray(sponza, builder):
 
 
 @pytest.mark.parametrize("far", [False, True], ids=["grazing", "far-origin"])
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_shared_edge_rays_bit_exact(sponza, builder, far):
     from optixpathtracer_amd.renderer import setup_renderer
     from oracle.oracle import OracleScene
@@ -92,7 +92,7 @@ def test_shared_edge_rays_sphere_box_bit_exact():
 
 
 @pytest.mark.parametrize("scene_name", ["sphere_box_diffuse", "sponza_class"])
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_bvh_build_deterministic(scene_name, builder):
     """Two builds of one scene give the same node and triangle arrays bit for bit (BVH4 slots are
     numbered breadth-first by a prefix sum, not by atomic arrival order)."""

@@ -32,7 +32,7 @@ def diffuse_scene():
     return scenes.sphere_in_box("diffuse")
 
 
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_trace_closest_bit_exact(diffuse_scene, builder):
     from optixpathtracer_amd.renderer import setup_renderer
     from oracle.oracle import OracleScene
@@ -56,7 +56,7 @@ def test_trace_closest_bit_exact(diffuse_scene, builder):
     r.close()
 
 
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_trace_sponza_class_bit_exact(builder):
     """~250k triangles: deeper trees, many PLOC iterations, LDS-stack spills."""
     from optixpathtracer_amd import scenes
@@ -84,7 +84,7 @@ def test_trace_sponza_class_bit_exact(builder):
     o.close()
 
 
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_trace_two_triangles(builder):
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import OptixRenderer
@@ -102,7 +102,7 @@ def test_trace_two_triangles(builder):
     r.close()
 
 
-@pytest.mark.parametrize("builder", [3, 1, 2], ids=["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("builder", [3, 1, 2, 4], ids=["ploc", "lbvh", "sah", "sah_gpu"])
 def test_trace_empty_and_single_triangle(builder):
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import OptixRenderer
@@ -544,7 +544,7 @@ def test_fullhd_largest_batch_bit_identical(diffuse_scene, mode):
     assert sr["samples"] == 1920 * 1080 * n
 
 
-@pytest.mark.parametrize("builder", [2, 3], ids=["sah", "ploc"])
+@pytest.mark.parametrize("builder", [2, 4, 3], ids=["sah", "sah_gpu", "ploc"])
 def test_degenerate_triangles_build_and_trace(builder):
     """Zero-area, duplicate-centroid and NaN-vertex triangles among valid ones: every builder
     finishes, and rays at the valid triangles hit them as the oracle says."""

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--budget", type=float, default=50.0)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--calls", type=int, default=70, help="calls after the synchronising stats read")
+    ap.add_argument("--mode", type=int, default=-1)
     a = ap.parse_args()
     import torch  # noqa: F401  (device init order as bench.py)
     from optixpathtracer_amd import scenes
@@ -29,6 +31,8 @@ def main():
     sc = scenes.make_scene(a.scene)
     r = setup_renderer(sc, a.width, a.height, a.depth)
     r.set_render_ahead_budget(a.budget)
+    if a.mode >= 0:
+        r.set_material_mode(a.mode)
     buf = np.empty((a.height, a.width, 3), np.float32)
     out = {"scene": a.scene, "budget_ms": a.budget, "rounds": []}
     for k in range(a.rounds):
@@ -39,7 +43,7 @@ def main():
             r.Render(buf)
         steady = (time.perf_counter() - t) / 200
         s0 = r.stats()  # synchronises: the look-ahead batch in flight completes
-        for _ in range(70):  # into the next look-ahead batch without a synchronising call
+        for _ in range(a.calls):  # into the next look-ahead batch without a synchronising call
             r.Render(buf)
         pos = np.asarray(sc.camera_blender_pos, np.float32) + np.float32(1e-3 * (k + 1))
         t = time.perf_counter()

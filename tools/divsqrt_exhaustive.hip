@@ -5,6 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/divsqrt_exhaustive.hip -o tools/divsqrt_exhaustive
 //   tools/divsqrt_exhaustive rcp          all 2^32 x: pt_rcp's fast path and its guard
 //   tools/divsqrt_exhaustive sqrt         all 2^32 x: pt_sqrt's fast path and its guard
+//   tools/divsqrt_exhaustive sqrtnb       all 2^32 x: pt_sqrt_nb (branchless)
 //   tools/divsqrt_exhaustive div EA EB    all 2^23 x 2^23 significand pairs of a in [2^EA, 2^EA+1),
 //                                         b in [2^EB, 2^EB+1) (EA / EB = -127: the denormal binade)
 //   tools/divsqrt_exhaustive divrand N    N * 2^30 random bit patterns (a, b), specials included
@@ -39,6 +40,15 @@ __global__ void k_rcp(Counters* c, unsigned long long base) {
         if (nb) atomicAdd(&c->bad, (unsigned long long)__popcll(nb));
         if (ns) atomicAdd(&c->slow, (unsigned long long)__popcll(ns));
     }
+    if (bad) atomicMin(&c->first_a, bits);
+}
+
+__global__ void k_sqrtnb(Counters* c, unsigned long long base) {  // the branchless variant, every input
+    const unsigned int bits = (unsigned int)(base + blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x);
+    const float x = __uint_as_float(bits);
+    const bool bad = !same_bits(pt::pt_sqrt_nb(x), sqrtf(x));
+    const unsigned long long nb = __ballot(bad);
+    if ((threadIdx.x & 63) == 0 && nb) atomicAdd(&c->bad, (unsigned long long)__popcll(nb));
     if (bad) atomicMin(&c->first_a, bits);
 }
 
@@ -129,13 +139,15 @@ int main(int argc, char** argv) {
     hipMemcpy(d, &init, sizeof init, hipMemcpyHostToDevice);
     Counters h;
     const char* mode = argv[1];
-    if (!strcmp(mode, "rcp") || !strcmp(mode, "sqrt")) {
+    if (!strcmp(mode, "rcp") || !strcmp(mode, "sqrt") || !strcmp(mode, "sqrtnb")) {
         const unsigned long long chunk = 1ull << 30;
         for (unsigned long long base = 0; base < (1ull << 32); base += chunk) {
             if (!strcmp(mode, "rcp"))
                 hipLaunchKernelGGL(k_rcp, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, d, base);
-            else
+            else if (!strcmp(mode, "sqrt"))
                 hipLaunchKernelGGL(k_sqrt, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, d, base);
+            else
+                hipLaunchKernelGGL(k_sqrtnb, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, d, base);
         }
         hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
         report(mode, h, 4294967296.0);
