@@ -13,10 +13,11 @@
 // collapse, the BVH4 are identical to PT_BVH_SAH's bit for bit (tests/test_gpu_sah_builder.py).
 // Only the internal node numbering differs, which the collapse never sees.
 //
-// Two phases.  Large nodes (more than kSmallMax triangles) are processed level by level, one
-// 512-thread workgroup per node: block reductions for the node and centroid boxes, bins in LDS
-// (ordered-int atomics), one wave per axis for the sweep, a tiled stable partition; the host reads
-// back the split positions of the level, numbers the children and launches the next level.
+// Two phases.  Large nodes (more than kSmallMax triangles) are processed level by level, each cut
+// into chunks of 4096 triangles with one workgroup per chunk: block reductions for the node and
+// centroid boxes and LDS bins (ordered-int atomics) merged into the node's with global atomics, one
+// wave per node for the sweep, a tiled stable partition after the node's earlier chunks; the host
+// reads back the split positions of the level, numbers the children and launches the next level.
 // Nodes of at most kSmallMax triangles are subtrees built to the end by one wave each: the same
 // steps at wave scale (wave-private LDS bins, shuffle scans for the sweep, ballot/mbcnt for the
 // partition), with the smaller child processed next and the larger one stacked, so the stack
@@ -35,9 +36,10 @@ namespace pt {
 namespace {
 
 constexpr int kSBins = 64;       // centroid bins per axis: pt_sah.cpp kBins
-constexpr int kSmallMax = 512;   // subtree size built by one wave
-constexpr int kLargeBlock = 512;  // 2 waves per SIMD: room for the sweep's registers
-constexpr int kLargeWaves = kLargeBlock / 64;
+#ifndef PT_SAH_SMALL
+#define PT_SAH_SMALL 64  // 512 / 128 / 64 / 32: 7.9 / 5.9 / 5.6 / 5.8 ms warm at 250k triangles
+#endif
+constexpr int kSmallMax = PT_SAH_SMALL;  // subtree size built by one wave
 constexpr int kSmallBlock = 256;
 constexpr int kSmallWaves = kSmallBlock / 64;
 constexpr int kSmallStack = 16;  // > log2(kSmallMax): the larger child is stacked, the smaller one goes on
@@ -155,36 +157,62 @@ __device__ int wave_sweep(const int* bins, int valid_axis) {
     return best_code;
 }
 
-// ---- large nodes: one 512-thread workgroup per node, one level per launch ------------------
+// ---- large nodes: one level per pass, several workgroups per node ---------------------------
+// A level's nodes are cut into chunks of kChunk consecutive triangles, one 256-thread workgroup
+// each: the node and centroid boxes and the bins are reduced per chunk in LDS and merged into the
+// node's global copy with atomics (min / max / add: exact and order-independent), one wave per
+// node takes the split decision, and the stable partition writes every chunk's left triangles
+// after the left triangles of the node's earlier chunks (a prefix over the chunks' counts).
 struct LargeNode {
     int begin, end;  // [begin, end) of the level's source order buffer
     int id;          // binary node id
+    int chunk0;      // its first chunk
 };
+struct Chunk {
+    int node, begin, end;
+};
+constexpr int kChunk = 4096;
+constexpr int kChunkBlock = 256;
+constexpr int kChunkWaves = kChunkBlock / 64;
+constexpr int kAcc = 12;                // node box lo / hi, centroid box lo / hi (ordered ints)
+constexpr int kBinInts = 3 * kSBins * 8;  // lo xyz, hi xyz, count, pad per bin
 
-__device__ __forceinline__ int block_sum(int v, int* lds) {  // every thread gets the block total
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    const int wave = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) lds[wave] = v;
-    __syncthreads();
-    int t = 0;
-    for (int w = 0; w < kLargeWaves; ++w) t += lds[w];
-    return t;
+__global__ void k_lg_init(int nn, int* acc, int* bins) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nn * kAcc) {
+        const int k = i % kAcc;
+        acc[i] = (k % 6) < 3 ? f2o(FLT_MAX) : f2o(-FLT_MAX);
+    }
+    if (i < nn * kBinInts) {
+        const int f = i & 7;
+        bins[i] = f < 3 ? f2o(FLT_MAX) : f < 6 ? f2o(-FLT_MAX) : 0;
+    }
 }
 
-__global__ __launch_bounds__(kLargeBlock) void k_sah_large(SahTris T, SahOut O, const LargeNode* nodes,
-                                                           const uint32_t* src, uint32_t* dst, int* mid_out) {
-    const LargeNode nd = nodes[blockIdx.x];
-    const int m = nd.end - nd.begin;
-    __shared__ int s_box[kLargeWaves][12];    // per wave: node box lo/hi, centroid box lo/hi (ordered ints)
-    __shared__ int s_bins[3 * kSBins * 8];    // lo xyz, hi xyz, count, pad per bin
-    __shared__ int s_red[kLargeWaves];
-    __shared__ int s_split;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // node box and centroid box (pt_sah.cpp: nb.grow(tb), cb.grow(cen) over the range)
+__device__ __forceinline__ void block_reduce_acc(int ob[kAcc], int (*lds)[kAcc]) {
+    for (int o = 32; o >= 1; o >>= 1)
+        for (int k = 0; k < kAcc; ++k) {
+            const int v = __shfl_xor(ob[k], o, 64);
+            ob[k] = (k % 6) < 3 ? min(ob[k], v) : max(ob[k], v);
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < kAcc; ++k) lds[threadIdx.x >> 6][k] = ob[k];
+    __syncthreads();
+    for (int k = 0; k < kAcc; ++k) {
+        int v = lds[0][k];
+        for (int w = 1; w < kChunkWaves; ++w) v = (k % 6) < 3 ? min(v, lds[w][k]) : max(v, lds[w][k]);
+        ob[k] = v;
+    }
+}
+
+// node box and centroid box of each chunk, merged into the node's (pt_sah.cpp nb / cb)
+__global__ __launch_bounds__(kChunkBlock) void k_lg_bounds(SahTris T, const Chunk* chunks, const uint32_t* src,
+                                                           int* acc) {
+    const Chunk ch = chunks[blockIdx.x];
+    __shared__ int s_red[kChunkWaves][kAcc];
     float nb[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
     float cb[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
-    for (int k = nd.begin + (int)threadIdx.x; k < nd.end; k += kLargeBlock) {
+    for (int k = ch.begin + (int)threadIdx.x; k < ch.end; k += kChunkBlock) {
         const uint32_t t = src[k];
         const float4 l = T.tlo[t], h = T.thi[t], c = T.cen[t];
         nb[0] = gmin_h(nb[0], l.x); nb[1] = gmin_h(nb[1], l.y); nb[2] = gmin_h(nb[2], l.z);
@@ -192,45 +220,53 @@ __global__ __launch_bounds__(kLargeBlock) void k_sah_large(SahTris T, SahOut O, 
         cb[0] = gmin_h(cb[0], c.x); cb[1] = gmin_h(cb[1], c.y); cb[2] = gmin_h(cb[2], c.z);
         cb[3] = gmax_h(cb[3], c.x); cb[4] = gmax_h(cb[4], c.y); cb[5] = gmax_h(cb[5], c.z);
     }
-    int ob[12];
+    int ob[kAcc];
     for (int k = 0; k < 6; ++k) {
         ob[k] = f2o(nb[k]);
         ob[6 + k] = f2o(cb[k]);
     }
-    for (int o = 32; o >= 1; o >>= 1)
-        for (int k = 0; k < 12; ++k) {
-            const int v = __shfl_xor(ob[k], o, 64);
-            ob[k] = (k % 6) < 3 ? min(ob[k], v) : max(ob[k], v);
+    block_reduce_acc(ob, s_red);
+    if (threadIdx.x < kAcc) {
+        const int k = threadIdx.x;
+        int v = ob[0];
+        for (int j = 1; j < kAcc; ++j) v = j == k ? ob[j] : v;  // ob[k] without dynamic indexing
+        if ((k % 6) < 3) atomicMin(acc + ch.node * kAcc + k, v);
+        else atomicMax(acc + ch.node * kAcc + k, v);
+    }
+}
+
+// the axes with a usable centroid extent, their lower bound and bin scale (pt_sah.cpp)
+__device__ __forceinline__ int axis_setup(const int* a, float clo[3], float scale[3]) {
+    int valid = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        clo[k] = o2f(a[6 + k]);
+        const float ext = o2f(a[9 + k]) - clo[k];
+        scale[k] = 1.0f;
+        if (ext > 0.0f && isfinite(ext)) {
+            valid |= 1 << k;
+            scale[k] = (float)kSBins / ext;
         }
-    if (lane == 0)
-        for (int k = 0; k < 12; ++k) s_box[wave][k] = ob[k];
-    for (int i = threadIdx.x; i < 3 * kSBins * 8; i += kLargeBlock) {
+    }
+    return valid;
+}
+
+__global__ __launch_bounds__(kChunkBlock) void k_lg_bins(SahTris T, const Chunk* chunks, const uint32_t* src,
+                                                         const int* acc, int* bins) {
+    const Chunk ch = chunks[blockIdx.x];
+    __shared__ int s_bins[kBinInts];
+    float clo[3], scale[3];
+    const int valid = axis_setup(acc + ch.node * kAcc, clo, scale);
+    for (int i = threadIdx.x; i < kBinInts; i += kChunkBlock) {
         const int f = i & 7;
         s_bins[i] = f < 3 ? f2o(FLT_MAX) : f < 6 ? f2o(-FLT_MAX) : 0;
     }
     __syncthreads();
-    for (int k = 0; k < 12; ++k) {
-        int v = s_box[0][k];
-        for (int w = 1; w < kLargeWaves; ++w) v = (k % 6) < 3 ? min(v, s_box[w][k]) : max(v, s_box[w][k]);
-        ob[k] = v;
-    }
-    float clo[3], scale[3];
-    int valid = 0;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        clo[a] = o2f(ob[6 + a]);
-        const float ext = o2f(ob[9 + a]) - clo[a];
-        scale[a] = 1.0f;
-        if (ext > 0.0f && isfinite(ext)) {
-            valid |= 1 << a;
-            scale[a] = (float)kSBins / ext;
-        }
-    }
-    // bins of the valid axes
-    for (int k = nd.begin + (int)threadIdx.x; k < nd.end; k += kLargeBlock) {
+    for (int k = ch.begin + (int)threadIdx.x; k < ch.end; k += kChunkBlock) {
         const uint32_t t = src[k];
         const float4 l = T.tlo[t], h = T.thi[t], c = T.cen[t];
         const float cc[3] = {c.x, c.y, c.z};
+#pragma unroll
         for (int a = 0; a < 3; ++a) {
             if (!((valid >> a) & 1)) continue;
             int* b = s_bins + (a * kSBins + bin_of(cc[a], clo[a], scale[a])) * 8;
@@ -240,67 +276,127 @@ __global__ __launch_bounds__(kLargeBlock) void k_sah_large(SahTris T, SahOut O, 
         }
     }
     __syncthreads();
-    if (wave == 0) {
-        const int code = wave_sweep(s_bins, valid);
-        if (lane == 0) s_split = code;
+    int* g = bins + (size_t)ch.node * kBinInts;
+    for (int i = threadIdx.x; i < 3 * kSBins; i += kChunkBlock) {
+        const int* b = s_bins + i * 8;
+        if (b[6] == 0) continue;  // an empty bin adds nothing to the union
+        int* d = g + i * 8;
+        atomicMin(d + 0, b[0]); atomicMin(d + 1, b[1]); atomicMin(d + 2, b[2]);
+        atomicMax(d + 3, b[3]); atomicMax(d + 4, b[4]); atomicMax(d + 5, b[5]);
+        atomicAdd(d + 6, b[6]);
     }
-    __syncthreads();
-    const int code = s_split;
-    const int axis = code >= 0 ? code / kSBins : 0, split = code >= 0 ? code % kSBins : 0;
-    const float lo_ax = axis == 0 ? clo[0] : axis == 1 ? clo[1] : clo[2];  // no dynamic indexing (scratch)
-    const float sc_ax = axis == 0 ? scale[0] : axis == 1 ? scale[1] : scale[2];
-    // left count, then the tiled stable partition
-    int nl_part = 0;
-    if (code >= 0)
-        for (int k = nd.begin + (int)threadIdx.x; k < nd.end; k += kLargeBlock) {
-            const float4 c = T.cen[src[k]];
-            const float ca = axis == 0 ? c.x : axis == 1 ? c.y : c.z;
-            nl_part += bin_of(ca, lo_ax, sc_ax) <= split ? 1 : 0;
-        }
-    const int nl = code >= 0 ? block_sum(nl_part, s_red) : 0;
-    const bool cut_middle = code < 0 || nl == 0 || nl == m;
-    const int mid = cut_middle ? nd.begin + m / 2 : nd.begin + nl;
-    if (threadIdx.x == 0) {
-        mid_out[blockIdx.x] = mid;
+}
+
+// one wave per node: the split decision, the node's box and range
+__global__ void k_lg_sweep(SahOut O, const LargeNode* nodes, int nn, const int* acc, const int* bins, int* code) {
+    const int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (i >= nn) return;
+    const int* a = acc + i * kAcc;
+    float clo[3], scale[3];
+    const int valid = axis_setup(a, clo, scale);
+    const int c = wave_sweep(bins + (size_t)i * kBinInts, valid);
+    if ((threadIdx.x & 63) == 0) {
+        const LargeNode nd = nodes[i];
+        code[i] = c;
         O.range[nd.id] = make_int2(nd.begin, nd.end - 1);
-        O.box[2 * (size_t)nd.id] = make_float4(o2f(ob[0]), o2f(ob[1]), o2f(ob[2]), 0.0f);
-        O.box[2 * (size_t)nd.id + 1] = make_float4(o2f(ob[3]), o2f(ob[4]), o2f(ob[5]), 0.0f);
+        O.box[2 * (size_t)nd.id] = make_float4(o2f(a[0]), o2f(a[1]), o2f(a[2]), 0.0f);
+        O.box[2 * (size_t)nd.id + 1] = make_float4(o2f(a[3]), o2f(a[4]), o2f(a[5]), 0.0f);
     }
-    int lbase = nd.begin, rbase = mid;
-    for (int k0 = nd.begin; k0 < nd.end; k0 += kLargeBlock) {  // block-uniform trip count
+}
+
+__device__ __forceinline__ bool goes_left(const SahTris& T, uint32_t t, int axis, float lo, float sc, int split) {
+    const float4 c = T.cen[t];
+    const float ca = axis == 0 ? c.x : axis == 1 ? c.y : c.z;
+    return bin_of(ca, lo, sc) <= split;
+}
+__device__ __forceinline__ void split_of(const int* acc, int code, int& axis, int& split, float& lo, float& sc) {
+    float clo[3], scale[3];
+    (void)axis_setup(acc, clo, scale);
+    axis = code >= 0 ? code / kSBins : 0;
+    split = code >= 0 ? code % kSBins : 0;
+    lo = axis == 0 ? clo[0] : axis == 1 ? clo[1] : clo[2];  // no dynamic indexing (scratch)
+    sc = axis == 0 ? scale[0] : axis == 1 ? scale[1] : scale[2];
+}
+
+__device__ __forceinline__ int block_total(int v, int* lds) {  // every thread gets the block total
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < kChunkWaves; ++w) t += lds[w];
+    return t;
+}
+
+__global__ __launch_bounds__(kChunkBlock) void k_lg_count(SahTris T, const Chunk* chunks, const uint32_t* src,
+                                                          const int* acc, const int* code, int* chunk_left) {
+    const Chunk ch = chunks[blockIdx.x];
+    __shared__ int s_red[kChunkWaves];
+    const int cd = code[ch.node];
+    int axis, split;
+    float lo, sc;
+    split_of(acc + ch.node * kAcc, cd, axis, split, lo, sc);
+    int n = 0;
+    if (cd >= 0)
+        for (int k = ch.begin + (int)threadIdx.x; k < ch.end; k += kChunkBlock)
+            n += goes_left(T, src[k], axis, lo, sc, split) ? 1 : 0;
+    n = block_total(n, s_red);
+    if (threadIdx.x == 0) chunk_left[blockIdx.x] = n;
+}
+
+// Stable partition of each chunk into dst; a node with no usable split is cut in the middle of its
+// range and copied unchanged.
+__global__ __launch_bounds__(kChunkBlock) void k_lg_scatter(SahTris T, const LargeNode* nodes, const Chunk* chunks,
+                                                            const uint32_t* src, uint32_t* dst, const int* acc,
+                                                            const int* code, const int* chunk_left, int* mid_out) {
+    const Chunk ch = chunks[blockIdx.x];
+    const LargeNode nd = nodes[ch.node];
+    __shared__ int s_cnt[kChunkWaves][2];
+    const int cd = code[ch.node];
+    int axis, split;
+    float lo, sc;
+    split_of(acc + ch.node * kAcc, cd, axis, split, lo, sc);
+    int loff = 0, nl = 0;  // left triangles of the node's earlier chunks, of all its chunks
+    for (int c = nd.chunk0; chunks[c].node == ch.node; ++c) {
+        if (c == (int)blockIdx.x) loff = nl;
+        nl += chunk_left[c];
+        if (chunks[c].end == nd.end) break;
+    }
+    const int m = nd.end - nd.begin;
+    const bool cut_middle = cd < 0 || nl == 0 || nl == m;
+    const int mid = cut_middle ? nd.begin + m / 2 : nd.begin + nl;
+    if (threadIdx.x == 0 && (int)blockIdx.x == nd.chunk0) mid_out[ch.node] = mid;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int lbase = nd.begin + loff, rbase = mid + (ch.begin - nd.begin - loff);
+    for (int k0 = ch.begin; k0 < ch.end; k0 += kChunkBlock) {  // block-uniform trip count
         const int k = k0 + (int)threadIdx.x;
-        const bool in = k < nd.end;
+        const bool in = k < ch.end;
         const uint32_t t = in ? src[k] : 0u;
-        bool left = false;
-        if (in && !cut_middle) {
-            const float4 c = T.cen[t];
-            const float ca = axis == 0 ? c.x : axis == 1 ? c.y : c.z;
-            left = bin_of(ca, lo_ax, sc_ax) <= split;
+        if (cut_middle) {
+            if (in) dst[k] = t;
+            continue;  // block-uniform
         }
+        const bool left = in && goes_left(T, t, axis, lo, sc, split);
         const unsigned long long ml = __ballot(in && left), mr = __ballot(in && !left);
         __syncthreads();
         if (lane == 0) {
-            s_box[wave][0] = __popcll(ml);
-            s_box[wave][1] = __popcll(mr);
+            s_cnt[wave][0] = __popcll(ml);
+            s_cnt[wave][1] = __popcll(mr);
         }
         __syncthreads();
         int pl = 0, pr = 0, tl = 0, tr = 0;
-        for (int w = 0; w < kLargeWaves; ++w) {
+        for (int w = 0; w < kChunkWaves; ++w) {
             if (w < wave) {
-                pl += s_box[w][0];
-                pr += s_box[w][1];
+                pl += s_cnt[w][0];
+                pr += s_cnt[w][1];
             }
-            tl += s_box[w][0];
-            tr += s_box[w][1];
+            tl += s_cnt[w][0];
+            tr += s_cnt[w][1];
         }
         if (in) {
-            if (cut_middle) {
-                dst[k] = t;
-            } else {
-                const unsigned long long mm = left ? ml : mr;
-                const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-                dst[left ? lbase + pl + r : rbase + pr + r] = t;
-            }
+            const unsigned long long mm = left ? ml : mr;
+            const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+            dst[left ? lbase + pl + r : rbase + pr + r] = t;
         }
         lbase += tl;
         rbase += tr;
@@ -480,10 +576,12 @@ hipError_t sah_build_gpu(const float4* tri, int n, uint32_t* order, int2* child,
     float4 *tlo = nullptr, *thi = nullptr, *cen = nullptr;
     uint32_t *buf[2] = {nullptr, nullptr};
     LargeNode* d_large = nullptr;
+    Chunk* d_chunks = nullptr;
     SmallTree* d_small = nullptr;
-    int* d_mid = nullptr;
+    int *d_mid = nullptr, *d_acc = nullptr, *d_bins = nullptr, *d_code = nullptr, *d_cleft = nullptr;
     int2* d_fix = nullptr;
     std::vector<LargeNode> level;
+    std::vector<Chunk> chunks;
     std::vector<SmallTree> small;
     std::vector<int> mids;
     std::vector<int2> fix;  // per large node: (id, 0), (child code 0, child code 1), written at the end
@@ -496,23 +594,50 @@ hipError_t sah_build_gpu(const float4* tri, int n, uint32_t* order, int2* child,
     alloc((void**)&cen, sizeof(float4) * (size_t)n);
     alloc((void**)&buf[0], sizeof(uint32_t) * (size_t)n);
     alloc((void**)&buf[1], sizeof(uint32_t) * (size_t)n);
-    alloc((void**)&d_mid, sizeof(int) * (size_t)n);
-    alloc((void**)&d_large, sizeof(LargeNode) * (size_t)n);
+    {
+        // a level holds at most n / (kSmallMax + 1) nodes, and a node of m triangles m / kChunk + 1 chunks
+        const size_t max_nodes = (size_t)n / (kSmallMax + 1) + 1, max_chunks = (size_t)n / kChunk + max_nodes;
+        alloc((void**)&d_mid, sizeof(int) * max_nodes);
+        alloc((void**)&d_code, sizeof(int) * max_nodes);
+        alloc((void**)&d_acc, sizeof(int) * kAcc * max_nodes);
+        alloc((void**)&d_bins, sizeof(int) * kBinInts * max_nodes);
+        alloc((void**)&d_large, sizeof(LargeNode) * max_nodes);
+        alloc((void**)&d_chunks, sizeof(Chunk) * max_chunks);
+        alloc((void**)&d_cleft, sizeof(int) * max_chunks);
+    }
     if (err != hipSuccess) goto done;
     hipLaunchKernelGGL(k_sah_prep, dim3((n + 255) / 256), dim3(256), 0, stream, tri, n, tlo, thi, cen, buf[0]);
     if ((err = hipGetLastError()) != hipSuccess) goto done;
     {
         const SahTris T{tlo, thi, cen};
         const SahOut O{child, range, box, order};
-        if (n > kSmallMax) level.push_back(LargeNode{0, n, 0});
+        if (n > kSmallMax) level.push_back(LargeNode{0, n, 0, 0});
         else small.push_back(SmallTree{0, n, 0, 0});
         while (!level.empty()) {
             const int nn = (int)level.size();
+            chunks.clear();
+            for (int i = 0; i < nn; ++i) {
+                level[i].chunk0 = (int)chunks.size();
+                for (int b = level[i].begin; b < level[i].end; b += kChunk)
+                    chunks.push_back(Chunk{i, b, std::min(level[i].end, b + kChunk)});
+            }
+            const int nc = (int)chunks.size();
             if ((err = hipMemcpyAsync(d_large, level.data(), sizeof(LargeNode) * nn, hipMemcpyHostToDevice, stream)) !=
-                hipSuccess)
+                    hipSuccess ||
+                (err = hipMemcpyAsync(d_chunks, chunks.data(), sizeof(Chunk) * nc, hipMemcpyHostToDevice, stream)) !=
+                    hipSuccess)
                 goto done;
-            hipLaunchKernelGGL(k_sah_large, dim3(nn), dim3(kLargeBlock), 0, stream, T, O, d_large, buf[parity],
-                               buf[1 - parity], d_mid);
+            const uint32_t* src = buf[parity];
+            uint32_t* dst = buf[1 - parity];
+            hipLaunchKernelGGL(k_lg_init, dim3((nn * kBinInts + 255) / 256), dim3(256), 0, stream, nn, d_acc, d_bins);
+            hipLaunchKernelGGL(k_lg_bounds, dim3(nc), dim3(kChunkBlock), 0, stream, T, d_chunks, src, d_acc);
+            hipLaunchKernelGGL(k_lg_bins, dim3(nc), dim3(kChunkBlock), 0, stream, T, d_chunks, src, d_acc, d_bins);
+            hipLaunchKernelGGL(k_lg_sweep, dim3((nn + 3) / 4), dim3(256), 0, stream, O, d_large, nn, d_acc, d_bins,
+                               d_code);
+            hipLaunchKernelGGL(k_lg_count, dim3(nc), dim3(kChunkBlock), 0, stream, T, d_chunks, src, d_acc, d_code,
+                               d_cleft);
+            hipLaunchKernelGGL(k_lg_scatter, dim3(nc), dim3(kChunkBlock), 0, stream, T, d_large, d_chunks, src, dst,
+                               d_acc, d_code, d_cleft, d_mid);
             if ((err = hipGetLastError()) != hipSuccess) goto done;
             mids.resize(nn);
             if ((err = hipMemcpyAsync(mids.data(), d_mid, sizeof(int) * nn, hipMemcpyDeviceToHost, stream)) != hipSuccess)
@@ -531,7 +656,7 @@ hipError_t sah_build_gpu(const float4* tri, int n, uint32_t* order, int2* child,
                         small.push_back(SmallTree{b0[s], e0[s], -1, 1 - parity});
                     } else if (sz > kSmallMax) {
                         codes[s] = next_id++;
-                        next.push_back(LargeNode{b0[s], e0[s], codes[s]});
+                        next.push_back(LargeNode{b0[s], e0[s], codes[s], 0});
                     } else {
                         codes[s] = next_id;
                         small.push_back(SmallTree{b0[s], e0[s], next_id, 1 - parity});
@@ -572,7 +697,8 @@ hipError_t sah_build_gpu(const float4* tri, int n, uint32_t* order, int2* child,
 done:
     (void)hipStreamSynchronize(stream);
     for (void* p : {(void*)tlo, (void*)thi, (void*)cen, (void*)buf[0], (void*)buf[1], (void*)d_large, (void*)d_small,
-                    (void*)d_mid, (void*)d_fix})
+                    (void*)d_mid, (void*)d_fix, (void*)d_chunks, (void*)d_acc, (void*)d_bins, (void*)d_code,
+                    (void*)d_cleft})
         if (p) (void)hipFree(p);
     return err;
 }

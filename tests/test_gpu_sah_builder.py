@@ -3,7 +3,7 @@ host builder it restates (PT_BVH_SAH, pt_sah.cpp): the downloaded BVH4 nodes and
 triangle records must be identical bit for bit -- the same binned-SAH decisions at every node, the
 same stable partitions and middle cuts, hence the same DFS leaf order and the same collapse.  Both
 replace optixAccelBuild (OptixRenderer.cpp:306-456).  Scenes cover both phases of the GPU build
-(large nodes level by level, subtrees of <= 512 triangles per wave) and the degenerate inputs the
+(large nodes level by level, subtrees of <= 64 triangles per wave) and the degenerate inputs the
 host build handles (coincident centroids, points, segments, NaN and infinite vertices)."""
 import numpy as np
 import pytest
@@ -58,9 +58,9 @@ def test_sponza_class_identical_and_fast():
     assert s_gpu["bvh_build_ms"] < 25.0, s_gpu["bvh_build_ms"]
 
 
-@pytest.mark.parametrize("n", [2, 3, 5, 64, 511, 512, 513, 1025, 5000])
+@pytest.mark.parametrize("n", [2, 3, 5, 31, 32, 33, 64, 65, 127, 128, 129, 511, 512, 513, 1025, 5000])
 def test_random_soups_identical(n):
-    """Sizes at the phase boundaries (one wave builds subtrees of <= 512 triangles), clustered and
+    """Sizes at the phase boundaries (one wave builds subtrees of <= 64 triangles; PT_SAH_SMALL variants of 32-512 passed the same list), clustered and
     sliver triangles."""
     rng = np.random.default_rng(n)
     c = rng.normal(size=(n, 1, 3)).astype(np.float32) * np.float32(3)
