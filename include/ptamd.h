@@ -174,6 +174,11 @@ typedef struct pt_stats {
     uint64_t pair_kernel_launches;
     uint64_t pair_kernel_rays;
     uint64_t pair_kernel_bytes;
+    /* the shadow rays among pair_kernel_rays (the rest are extension rays), and the shadow rays of
+       k_trace_pair that found their light unoccluded (each adds its contribution to the path's
+       radiance: a 16-B read and write; counted while pt_set_traversal_stats(r, 1)) */
+    uint64_t pair_kernel_shadow_rays;
+    uint64_t nee_unoccluded;
 } pt_stats;
 
 typedef struct pt_renderer pt_renderer;

@@ -136,6 +136,8 @@ class pt_stats(C.Structure):
         ("pair_kernel_launches", C.c_uint64),
         ("pair_kernel_rays", C.c_uint64),
         ("pair_kernel_bytes", C.c_uint64),
+        ("pair_kernel_shadow_rays", C.c_uint64),
+        ("nee_unoccluded", C.c_uint64),
     ]
 
 

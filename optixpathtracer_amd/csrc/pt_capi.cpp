@@ -90,7 +90,7 @@ struct EventPool {
 // [9..13] wave schedule of the trace kernels (pt_stats wave_*) [14] node visits served from LDS
 // [15] items of the timed shading kernel (pt_stats shade_kernel_items) [16] [17] rays and
 // algorithmic bytes of the k_trace_pair launches alone (pt_stats pair_kernel_*).
-constexpr int kCounters = 18;
+constexpr int kCounters = 20;
 // event pairs held by one renderer before launch_frames retires them (EventPool)
 constexpr size_t kMaxPendingEvents = 4096;
 // the smallest traversal stack of any kernel (pt_device.h stack_capacity: 71 entries for the
@@ -1517,6 +1517,8 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->look_ahead_cancelled = r->ahead_cancelled;
     out->pair_kernel_rays = c[16];
     out->pair_kernel_bytes = c[17];
+    out->pair_kernel_shadow_rays = c[19];
+    out->nee_unoccluded = c[18];
     // a multi-device renderer reports the work of all its devices (times are device 0's)
     for (pt_renderer* p : r->peers) {
         pt_stats ps;
@@ -1539,6 +1541,7 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
         out->trace_kernel_rays += ps.trace_kernel_rays;
         out->trace_kernel_bytes += ps.trace_kernel_bytes;
         out->strict_retraces += ps.strict_retraces;
+        out->nee_unoccluded += ps.nee_unoccluded;
     }
     return PT_OK;
 }

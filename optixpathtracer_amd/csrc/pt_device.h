@@ -126,6 +126,7 @@ __device__ __forceinline__ uint64_t probe_clock(const T& dep) {  // once `dep` i
 struct TravStats {
     uint32_t nodes = 0, tris = 0, rays = 0, overflow = 0, retrace = 0;
     uint32_t lds_nodes = 0;  // node visits served from the staged top levels (stage_top_nodes)
+    uint32_t unocc = 0;      // k_trace_pair: shadow rays that found their light unoccluded
     // wave schedule (trace_range, lane 0 of each wave): iterations, active lanes summed over
     // them, iterations running the node half / the triangle half, refill blocks
     uint32_t steps = 0, active = 0, node_steps = 0, tri_steps = 0, refills = 0;

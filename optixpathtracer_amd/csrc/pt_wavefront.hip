@@ -122,7 +122,7 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
     if (!STATS || !counters) return;
     const unsigned long long a = wave_sum_u64(ts.nodes), c = wave_sum_u64(ts.tris), d = wave_sum_u64(ts.rays);
     const unsigned long long e = wave_sum_u64(ts.overflow), r = wave_sum_u64(ts.retrace);
-    const unsigned long long l = wave_sum_u64(ts.lds_nodes);
+    const unsigned long long l = wave_sum_u64(ts.lds_nodes), u = wave_sum_u64(ts.unocc);
     if (lane_id() == 0) {  // the wave-schedule counts are kept by every lane alike: lane 0's
         atomicAdd(&counters[1], a);
         atomicAdd(&counters[2], c);
@@ -135,6 +135,7 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
         atomicAdd(&counters[12], (unsigned long long)ts.tri_steps);
         atomicAdd(&counters[13], (unsigned long long)ts.refills);
         atomicAdd(&counters[14], l);
+        atomicAdd(&counters[18], u);
     }
 }
 
@@ -341,6 +342,23 @@ __device__ __forceinline__ float4 ldqs(const float4* p) {
 }
 __device__ __forceinline__ void stqs(float4* p, float4 v) {
     __builtin_nontemporal_store(pt_v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<pt_v4f*>(p));
+}
+
+// k_trace_pair's queue records (DESIGN.md §5 "Where k_trace_pair's memory traffic goes"):
+// PT_TRACE_NTQ = 1 loads and stores them non-temporally; PT_PROBE_NO_NEE_ADD = 1 drops the deferred
+// NEE add (a measurement probe: wrong images, same rays).
+#ifndef PT_TRACE_NTQ
+#define PT_TRACE_NTQ 0
+#endif
+#ifndef PT_PROBE_NO_NEE_ADD
+#define PT_PROBE_NO_NEE_ADD 0
+#endif
+__device__ __forceinline__ float4 ldq_pair(const float4* p) { return PT_TRACE_NTQ ? ldqs(p) : *p; }
+__device__ __forceinline__ void stq_pair(float4* p, float4 v) {
+    if (PT_TRACE_NTQ)
+        stqs(p, v);
+    else
+        *p = v;
 }
 
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
@@ -790,16 +808,16 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
     TravStats ts;
     auto fetch = [&](int i, TravState& st) {
         if (i < n_ext) {
-            const float4 a = ro[i], c = rd[i];
+            const float4 a = ldq_pair(ro + i), c = ldq_pair(rd + i);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
             st.path = __float_as_int(a.w);
         } else {
             const int j = i - n_ext;
-            const float4 c = W.sh_d[j], k = W.sh_c[j];
+            const float4 c = ldq_pair(W.sh_d + j), k = ldq_pair(W.sh_c + j);
             // origin | path: the shadow ray's own record, or (Lambert) the continuation ray of the
             // same path, which starts at the same point (k_shade_fused)
             const int q = __float_as_int(k.w);
-            const float4 a = q >= 0 ? ro[q] : W.sh_o[j];
+            const float4 a = ldq_pair(q >= 0 ? ro + q : W.sh_o + j);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
             st.any = true;
             // an any-hit traversal only writes h.tri: the record's other fields carry the path
@@ -822,9 +840,10 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
         NeeAdd a{nullptr, make_float4(0.0f, 0.0f, 0.0f, 0.0f), 0.0f, 0.0f, 0.0f};
         const Hit& h = st.h;
         // the hit-record stores first: a store issued after the radiance load would wait for it
-        if (i < n_ext) W.hit[i] = hit_record(h, st.path);
+        if (i < n_ext) stq_pair(W.hit + i, hit_record(h, st.path));
         __builtin_amdgcn_sched_barrier(0);
-        if (i >= n_ext && h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+        if (STATS && i >= n_ext && h.tri < 0) ts.unocc++;
+        if (!PT_PROBE_NO_NEE_ADD && i >= n_ext && h.tri < 0) {  // unoccluded: add the deferred NEE contribution
             a.p = W.L + h.orig;
             a.v = *a.p;
             a.x = h.t;
@@ -861,6 +880,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
         atomicAdd(&counters[7], 48ull * (unsigned long long)(n_ext + n_sh));  // their queue bytes
         atomicAdd(&counters[16], (unsigned long long)(n_ext + n_sh));         // the same, k_trace_pair alone
         atomicAdd(&counters[17], 48ull * (unsigned long long)(n_ext + n_sh));
+        atomicAdd(&counters[19], (unsigned long long)n_sh);
     }
     flush_trav_stats<STATS>(counters, ts);
 }

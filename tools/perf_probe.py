@@ -115,6 +115,15 @@ def main():
                                     # raw counters (a PT_CYCLE_PROBE build puts shader cycles per section here)
                                     "raw": {k: s[k] for k in ("wave_steps", "wave_active_lanes", "wave_node_steps",
                                                               "wave_tri_steps", "wave_refills", "rays")}})
+                        # k_trace_pair per launch (the traffic classes of DESIGN.md §5): its rays, of
+                        # them shadow rays, unoccluded shadow rays; the node visits of all trace
+                        # kernels that loaded from global memory and their triangle tests
+                        pl = max(1, s["pair_kernel_launches"])
+                        out["pair_per_launch"] = {
+                            "rays": s["pair_kernel_rays"] / pl, "shadow_rays": s["pair_kernel_shadow_rays"] / pl,
+                            "unoccluded": s["nee_unoccluded"] / pl, "launches": s["pair_kernel_launches"],
+                            "all_trace_rays": s["rays"], "global_node_visits": s["nodes_visited"] - s["lds_nodes_visited"],
+                            "tri_tests": s["tri_tests"]}
                     print(json.dumps(out), flush=True)
         r.close()
 
