@@ -20,7 +20,9 @@ spp per step); the driver's default run is configs[1].
 Extra fields: `roofline` (HBM roofline of the mode's dominant kernel, measured with one HIP event
 pair per launch on the stream it runs on, per kernel: in the Lambert / Conductor / Dielectric modes
 k_trace_pair (the shadow rays of bounce b and the extension rays of b+1 of a 64-frame batch), 48
-algorithmic bytes per traced ray, ray read + result write; in the Default / Layered modes
+algorithmic bytes per traced ray (an extension ray's 32-B record read and 16-B hit record written,
+a shadow ray's three 16-B records read) plus 32 B (radiance read and write) per unoccluded shadow
+ray, whose share comes from the untimed traversal-statistics render; in the Default / Layered modes
 k_shade_nee, the layered NEE eval, 216 algorithmic bytes per item.  `window` says the timed
 region's launch windows are concurrent with the other wavefront stream's kernels (`single_stream`
 repeats the kernel alone); `binding` names the unit the PMC counters show binds the kernel -- the
@@ -52,6 +54,7 @@ BYTES_PER_TRACE = 48  # trace-kernel share per ray: ray record read 32 B + hit /
 # (isect v0 16 + shade 64) + material 32 + throughput|seed 16 + light index 4 + radiance RMW 32 +
 # seed write-back 16 (pt_wavefront.hip k_shade_nee)
 BYTES_PER_NEE_ITEM = 4 + 16 + 16 + 80 + 32 + 16 + 4 + 32 + 16
+NEE_ADD_BYTES = 32  # k_trace_pair: radiance read + write of an unoccluded shadow ray (W.L[path], 16 B each)
 CLOCK_HZ = 2.4e9  # MI355X shader clock (MI355X_MICROARCH.md; tools/td_probe.hip measured at 2400 MHz)
 N_CUS, N_SIMDS = 256, 1024
 # tools/td_probe.hip (profiles/r03s_td_probe.json): a 16-B-per-lane load costs the CU's texture
@@ -288,6 +291,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         e3 = float(t.item())
         value_other = (other, args.width * args.height * (args.spp * world if other == "weak" else args.spp) / e3 / 1e6)
+    # One more untimed render of two 64-frame batches with the traversal counters on (a separate
+    # kernel instance): node visits (global / from LDS), triangle tests and rays per trace launch,
+    # for the vector-memory roofline of the trace kernels (roofline.vmem).  Its time is not used.
+    trav = None
+    if args.kernel != 0:
+        r.set_traversal_stats(True)
+        r.stats_reset()
+        r.accum_clear()
+        r.render_frames(1, min(args.spp, 2 * args.frames_per_launch))
+        trav = r.stats()
+        r.set_traversal_stats(False)
+    # share of k_trace_pair's shadow rays that found their light unoccluded (each adds its
+    # contribution to the path radiance: NEE_ADD_BYTES more algorithmic bytes)
+    unocc_share = trav["nee_unoccluded"] / trav["pair_kernel_shadow_rays"] if trav and trav["pair_kernel_shadow_rays"] else 0.0
     # Transparency: the timed steps alternate the wavefront batches between two streams
     # (pt_set_wavefront_streams, default 2), so a trace launch shares the GPU with the other
     # batch's kernels and its event window is longer than its solo run.  One more step on a
@@ -312,7 +329,9 @@ def main():
             pair1 = s1["pair_kernel_launches"] > 0
             l1 = int(s1["pair_kernel_launches"] if pair1 else s1["trace_kernel_launches"])
             ms1 = (s1["pair_kernel_ms"] if pair1 else s1["trace_kernel_ms"]) / l1
-            ach1 = (s1["pair_kernel_bytes"] if pair1 else s1["trace_kernel_bytes"]) / l1 / (ms1 / 1e3) / 1e9
+            b1 = (s1["pair_kernel_bytes"] + NEE_ADD_BYTES * unocc_share * s1["pair_kernel_shadow_rays"]
+                  if pair1 else s1["trace_kernel_bytes"])
+            ach1 = b1 / l1 / (ms1 / 1e3) / 1e9
             s1_all_ms = s1["trace_kernel_ms"] / max(1, s1["trace_kernel_launches"])
             single = {"value": round(args.width * args.height * per_step_spp / e2 / 1e6, 3),
                       "kernel": "k_trace_pair" if pair1 else "k_extend",
@@ -321,17 +340,6 @@ def main():
                       "shade_avg_launch_ms": round(s1["shade_kernel_ms"] / max(1, s1["shade_kernel_launches"]), 4),
                       "shade_items_per_launch": s1["shade_kernel_items"] / max(1, s1["shade_kernel_launches"])}
         r.set_wavefront_streams(args.wavefront_streams)
-    # One more untimed render of two 64-frame batches with the traversal counters on (a separate
-    # kernel instance): node visits (global / from LDS), triangle tests and rays per trace launch,
-    # for the vector-memory roofline of the trace kernels (roofline.vmem).  Its time is not used.
-    trav = None
-    if args.kernel != 0:
-        r.set_traversal_stats(True)
-        r.stats_reset()
-        r.accum_clear()
-        r.render_frames(1, min(args.spp, 2 * args.frames_per_launch))
-        trav = r.stats()
-        r.set_traversal_stats(False)
     if rank == 0:
         nan_px = int(np.isnan(img).any(axis=-1).sum())
         kernel_s = st["total_render_ms"] / 1e3
@@ -343,7 +351,8 @@ def main():
             # (the batch's one k_extend is excluded), k_extend in Default / Layered
             pair = fused and st["pair_kernel_launches"] > 0
             launches = int(st["pair_kernel_launches"] if pair else st["trace_kernel_launches"])
-            t_bytes = (st["pair_kernel_bytes"] if pair else st["trace_kernel_bytes"]) / launches
+            t_bytes = (st["pair_kernel_bytes"] + NEE_ADD_BYTES * unocc_share * st["pair_kernel_shadow_rays"]
+                       if pair else st["trace_kernel_bytes"]) / launches
             t_s = (st["pair_kernel_ms"] if pair else st["trace_kernel_ms"]) / 1e3 / launches
             # all trace launches (k_extend + k_trace_pair): the denominator of the lane-load rate below
             all_s = st["trace_kernel_ms"] / 1e3 / int(st["trace_kernel_launches"])
@@ -384,9 +393,10 @@ def main():
             per_launch_bytes = trace_line["bytes_per_launch"]
             avg_launch_s = trace_line["avg_launch_ms"] / 1e3
             bytes_def = ("48 B per traced ray of one k_trace_pair launch (the shadow rays of bounce b and the "
-                         "extension rays of bounce b+1 of a 64-frame batch): the 32-B ray record read and one 16-B "
-                         "result, the hit record of an extension ray or the deferred radiance add of an "
-                         "unoccluded shadow ray")
+                         "extension rays of bounce b+1 of a 64-frame batch): an extension ray's 32-B record read "
+                         "and 16-B hit record written, a shadow ray's direction, contribution and origin records "
+                         f"read; plus {NEE_ADD_BYTES} B (radiance read + write) per unoccluded shadow ray "
+                         f"({unocc_share:.4f} of the shadow rays, traversal-statistics render)")
         elif st["shade_kernel_launches"] > 0:
             # Default / Layered: k_shade_nee (the stochastic layered NEE eval) takes 53-60 % of a frame
             # (DESIGN.md §8); its bound is VALU issue (roofline.valu), its HBM figure is reported too
@@ -410,13 +420,14 @@ def main():
         from optixpathtracer_amd.provenance import kernel_sources_sha
         sha = kernel_sources_sha()
         pmc_stale = {}
-        traffic = traffic_low = None
+        traffic = traffic_low = rd_sizes = None
         tjd, cur = pmc_record(Path(args.traffic_json), sha)
         if tjd and tjd.get("kernel") == dom and tjd.get("config", "2") == args.config:
             fig = {"hbm_bytes_per_launch": tjd.get("hbm_bytes_per_launch"),
                    "hbm_bytes_per_launch_low": tjd.get("hbm_bytes_per_launch_low")}
             if cur:
                 traffic, traffic_low = fig["hbm_bytes_per_launch"], fig["hbm_bytes_per_launch_low"]
+                rd_sizes = tjd.get("read_request_sizes")
             else:
                 pmc_stale["traffic"] = {**fig, "sources_sha": tjd.get("sources_sha"), "stale": True}
         valu = None  # the VALU fraction beside the HBM roofline, from PMC passes
@@ -528,6 +539,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic,
                 "traffic_low": traffic_low,
+                # the read requests by size (one more PMC pass): k_trace_pair reads whole 128-B lines,
+                # so `traffic` (2 x FETCH_SIZE + WRITE_SIZE) is the exact figure; its split into the
+                # queue records, BVH refetch, hit records and radiance adds: DESIGN.md §5
+                "traffic_read_requests": rd_sizes,
                 "kernel": dom,
                 "bytes_per_launch": int(per_launch_bytes),
                 "bytes_def": bytes_def,

@@ -348,10 +348,16 @@ __device__ __forceinline__ void stqs(float4* p, float4 v) {
 // PT_TRACE_NTQ = 1 loads and stores them non-temporally; PT_PROBE_NO_NEE_ADD = 1 drops the deferred
 // NEE add (a measurement probe: wrong images, same rays).
 #ifndef PT_TRACE_NTQ
-#define PT_TRACE_NTQ 0
+#define PT_TRACE_NTQ 1  // 19 % less k_trace_pair traffic, rate ±0.2 %
 #endif
 #ifndef PT_PROBE_NO_NEE_ADD
 #define PT_PROBE_NO_NEE_ADD 0
+#endif
+// How an unoccluded shadow ray of k_trace_pair adds its contribution to W.L[path]: 0 = load in
+// finish + store in commit (v37); 1 = three no-return float atomics; 2 = the ray only writes its
+// path (or -1) into its own sh_c record and k_nee_add adds in shadow-queue order after the launch.
+#ifndef PT_NEE_MODE
+#define PT_NEE_MODE 0
 #endif
 __device__ __forceinline__ float4 ldq_pair(const float4* p) { return PT_TRACE_NTQ ? ldqs(p) : *p; }
 __device__ __forceinline__ void stq_pair(float4* p, float4 v) {
@@ -843,9 +849,11 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
         if (i < n_ext) stq_pair(W.hit + i, hit_record(h, st.path));
         __builtin_amdgcn_sched_barrier(0);
         if (STATS && i >= n_ext && h.tri < 0) ts.unocc++;
-        if (!PT_PROBE_NO_NEE_ADD && i >= n_ext && h.tri < 0) {  // unoccluded: add the deferred NEE contribution
+        if (PT_NEE_MODE == 2 && !PT_PROBE_NO_NEE_ADD && i >= n_ext)  // k_nee_add adds
+            reinterpret_cast<int*>(W.sh_c + (i - n_ext))[3] = h.tri < 0 ? h.orig : -1;
+        if (PT_NEE_MODE != 2 && !PT_PROBE_NO_NEE_ADD && i >= n_ext && h.tri < 0) {  // unoccluded: add the deferred NEE contribution
             a.p = W.L + h.orig;
-            a.v = *a.p;
+            if (PT_NEE_MODE == 0) a.v = *a.p;
             a.x = h.t;
             a.y = h.u;
             a.z = h.v;
@@ -853,7 +861,14 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
         return a;
     };
     auto commit = [&](const NeeAdd& a) {
-        if (a.p) *a.p = make_float4(a.v.x + a.x, a.v.y + a.y, a.v.z + a.z, 0.0f);
+        if (PT_NEE_MODE == 1 && a.p) {
+            float* f = reinterpret_cast<float*>(a.p);
+            __hip_atomic_fetch_add(f + 0, a.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(f + 1, a.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(f + 2, a.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (a.p) {
+            *a.p = make_float4(a.v.x + a.x, a.v.y + a.y, a.v.z + a.z, 0.0f);
+        }
     };
 #else
     auto finish = [&](int i, const TravState& st) {
@@ -971,6 +986,21 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(false)) void k_shadow_vis(Dev
             const bool occluded = st.h.tri >= 0;
             W.vis[j] = table ? (occluded ? 0 : 1) : (occluded ? -1 : st.path);
         });
+}
+
+// PT_NEE_MODE 2: the unoccluded shadow rays of k_trace_pair(b) add their contributions to the
+// path radiance in shadow-queue order (sh_c[j] = contribution | path, or -1 when occluded).
+__global__ __launch_bounds__(kBlockWF) void k_nee_add(WFState W, int b) {
+    const int n = *cnt(W, b, kShadowQ);
+    if (wf_cancelled(W)) return;
+    for (int j = (int)(blockIdx.x * kBlockWF + threadIdx.x); j < n; j += (int)(gridDim.x * kBlockWF)) {
+        const float4 k = ldqs(W.sh_c + j);
+        const int p = __float_as_int(k.w);
+        if (p >= 0) {
+            const float4 l = W.L[p];
+            W.L[p] = make_float4(l.x + k.x, l.y + k.y, l.z + k.z, 0.0f);
+        }
+    }
 }
 
 // Visible shadow rays of bounce b -> the NEE bucket queues (vis[j] = item | bucket << 28, or -1).
@@ -1391,6 +1421,8 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
         ++timed;
+        if (PT_NEE_MODE == 2 && !PT_PROBE_NO_NEE_ADD)
+            hipLaunchKernelGGL(k_nee_add, dim3(8 * cus), dim3(kBlockWF), 0, stream, W, b);
         return hipGetLastError();
     };
     auto shadow_vis = [&](int b, int table) -> hipError_t {

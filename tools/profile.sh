@@ -23,6 +23,9 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
 echo "[profile] WRITE_SIZE"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
   python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check --reference-loops 0 $ARGS > "$OUT/write.json" 2> "$OUT/write.log"
+echo "[profile] read requests by size"
+timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --output-format csv -d "$OUT/rdsz" -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --spp 64 --no-cpu-baseline --no-dedup-check --reference-loops 0 $ARGS > "$OUT/rdsz.json" 2> "$OUT/rdsz.log"
 python3 tools/traffic.py "$OUT" > "$OUT/traffic.json"
 cat "$OUT/traffic.json"
 echo "[profile] done"

@@ -86,6 +86,18 @@ def main():
     w_kib = sum(write[kernel]) / len(write[kernel])
     hbm = 2.0 * f_kib * 1024.0 + w_kib * 1024.0
     low = f_kib * 1024.0 + w_kib * 1024.0
+    # read requests by size (tools/profile.sh `rdsz` pass): the read bytes without the half-count
+    # question -- k_trace_pair's are all 128-B requests (profiles/r05n_*), FETCH_SIZE tallies 64 B each
+    sizes = None
+    if (root / "rdsz").exists():
+        n = {c: per_kernel(root / "rdsz", c).get(kernel) for c in
+             ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")}
+        if all(n.values()):
+            m = {c: sum(v) / len(v) for c, v in n.items()}
+            rd = 32 * m["TCC_EA0_RDREQ_32B_sum"] + 64 * m["TCC_EA0_RDREQ_64B_sum"] + 128 * m["TCC_EA0_RDREQ_128B_sum"]
+            sizes = {"read_requests": round(m["TCC_EA0_RDREQ_sum"]), "of_them_128b": round(m["TCC_EA0_RDREQ_128B_sum"]),
+                     "of_them_64b": round(m["TCC_EA0_RDREQ_64B_sum"]), "of_them_32b": round(m["TCC_EA0_RDREQ_32B_sum"]),
+                     "read_bytes": int(rd), "hbm_bytes_per_launch_by_request_size": int(rd + w_kib * 1024.0)}
     print(json.dumps({
         "kernel": kernel,
         "dispatches": len(fetch[kernel]),
@@ -93,13 +105,15 @@ def main():
         "write_size_kib_mean": round(w_kib, 3),
         "hbm_bytes_per_launch": int(hbm),
         "hbm_bytes_per_launch_low": int(low),
+        "read_request_sizes": sizes,
         "kernel_trace": stats.get(kernel),
         # the same bench on one wavefront stream (tools/profile.sh kt1): solo launch times
         "kernel_trace_single_stream": kernel_stats(root / "kt1").get(kernel) if (root / "kt1").exists() else None,
         # the kernel sources these passes ran (bench.py reports the figures only on the same sources)
         "sources_sha": kernel_sources_sha(),
         "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB -> bytes; low: FETCH_SIZE + "
-                      "WRITE_SIZE (gathers are not half-counted, profiles/r02_hbm_calib.json)",
+                      "WRITE_SIZE (a lower bound only: read_request_sizes counts the requests by size, and "
+                      "where all are 128-B lines the first figure is exact)",
     }, indent=1))
 
 

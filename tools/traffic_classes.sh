@@ -2,7 +2,7 @@
 # Where k_trace_pair's memory traffic goes: PMC passes over
 # tools/perf_probe.py (Lambert, 1080p, 64 frames per batch) for libptamd variants, one rocprofv3 run
 # per counter group, plus a traversal-statistics run for the per-launch ray counts.
-#   tools/traffic_classes.sh OUTDIR "base noadd ntq"
+#   tools/traffic_classes.sh OUTDIR "base noadd ntq"    (SIZES_ONLY=1: the read-request size pass alone)
 set -e
 OUT=${1:-gpurun_out/tc}; VARS=${2:-base}
 ROOT="$GRAFT_REPO_ROOT"; [ -z "$ROOT" ] && ROOT=$(pwd)
@@ -15,6 +15,7 @@ for v in $VARS; do
     local name=$1; shift
     timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/${v}_$name" -o run -- python3 tools/perf_probe.py --repeat 1 --fpl 64 --spp 64 > "$OUT/${v}_$name.log" 2>&1
   }
+  if [ -n "$SIZES_ONLY" ]; then run tccsz TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_DRAM_sum; echo "$v done"; continue; fi
   timeout -k 10 240 python3 tools/perf_probe.py --repeat 1 --fpl 64 --spp 64 --stats > "$OUT/${v}_stats.log" 2>&1
   run fetch FETCH_SIZE
   run write WRITE_SIZE
