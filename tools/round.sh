@@ -51,5 +51,10 @@ else
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_config$cfg" -o run -- \
       python3 bench.py --config $cfg --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --reference-loops 0 \
       > "$OUT/kt_config$cfg.json" 2> "$OUT/kt_config$cfg.log"
+    # the same on one wavefront stream: solo kernel times (with two streams a short kernel's
+    # window includes the time its workgroups wait behind the other stream's kernels)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt1_config$cfg" -o run -- \
+      python3 bench.py --config $cfg --steps 1 --warmup 1 --no-cpu-baseline --no-dedup-check --reference-loops 0 \
+      --wavefront-streams 1 > "$OUT/kt1_config$cfg.json" 2> "$OUT/kt1_config$cfg.log"
   done
 fi

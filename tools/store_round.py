@@ -35,6 +35,8 @@ def main():
           (prof / "traffic.json", "traffic.json")]
     cp += [(rnd / f"kt_config{c}" / "run_kernel_stats.csv", f"{tag}_kernel_stats_config{c}.csv") for c in ("3", "5")
            if (rnd / f"kt_config{c}" / "run_kernel_stats.csv").exists()]
+    cp += [(rnd / f"kt1_config{c}" / "run_kernel_stats.csv", f"{tag}_kernel_stats_config{c}_single_stream.csv")
+           for c in ("3", "5") if (rnd / f"kt1_config{c}" / "run_kernel_stats.csv").exists()]
     for src, dst in cp:
         shutil.copyfile(src, out / dst)
     pmc = subprocess.run([sys.executable, str(ROOT / "tools" / "shade_pmc.py"),
