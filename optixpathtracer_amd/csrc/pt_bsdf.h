@@ -102,8 +102,18 @@ __device__ __forceinline__ float tr_pdf(f3 w, f3 wm, float alpha) {   // D(w, wm
 // G1(w) / |cos w|.  The layered walk computes them once per direction and reuses them across
 // its samples and depths; they are the same operations on the same inputs, so every result
 // stays bit-identical to recomputing them inline.
+// PT_TRDIR_LEAN = 1 keeps wh and T1 of the frame and recomputes T2 = cross(wh, T1) where a sample
+// uses it (the same operations, so the same bits): three registers fewer per direction the walk
+// holds.
+#ifndef PT_TRDIR_LEAN
+#define PT_TRDIR_LEAN 1
+#endif
 struct TRDir {
+#if PT_TRDIR_LEAN
+    f3 wh, T1;      // tr_sample_wm frame (tr_dir_frame); T2 = cross(wh, T1)
+#else
     f3 wh, T1, T2;  // tr_sample_wm frame (tr_dir_frame)
+#endif
     float lam;      // tr_lambda(w, alpha) (tr_dir_lam)
     float g1c;      // tr_G1(w, alpha) / abs_cos_theta(w) (tr_dir_lam)
 };
@@ -115,11 +125,17 @@ __device__ __forceinline__ void tr_dir_frame(TRDir& p, f3 w, float alpha) {  // 
     f3 wh = normalize(mk(alpha * w.x, alpha * w.y, w.z));
     if (wh.z < 0.0f) wh = -wh;
     p.T1 = (wh.z < 0.99999f) ? normalize(cross(mk(0.0f, 0.0f, 1.0f), wh)) : mk(1.0f, 0.0f, 0.0f);
+#if !PT_TRDIR_LEAN
     p.T2 = cross(wh, p.T1);
+#endif
     p.wh = wh;
 }
 __device__ __forceinline__ f3 tr_sample_wm_dir(uint32_t& seed, const TRDir& p, float alpha) {  // :99-119
+#if PT_TRDIR_LEAN
+    const f3 wh = p.wh, T1 = p.T1, T2 = cross(wh, T1);
+#else
     const f3 wh = p.wh, T1 = p.T1, T2 = p.T2;
+#endif
     float px, py;
     disk_polar(seed, px, py);
     float h = fsqrt(1.0f - sqr(px));
@@ -524,7 +540,25 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
     return mk(fdiv(b.color.x * c, b.pdf), fdiv(b.color.y * c, b.pdf), fdiv(b.color.z * c, b.pdf));
 }
 
-__device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+// PT_LAYERED_F_INLINE / PT_LAYERED_SAMPLE_INLINE = 1 inline the layered eval / sample walk into
+// their kernels (default; 0 = one call each)
+#ifndef PT_LAYERED_F_INLINE
+#define PT_LAYERED_F_INLINE 1  // with PT_LAYERED_SAMPLE_INLINE: Default +1.5 %, Sponza-class +1.2 %
+#endif
+#ifndef PT_LAYERED_SAMPLE_INLINE
+#define PT_LAYERED_SAMPLE_INLINE 1
+#endif
+#if PT_LAYERED_F_INLINE
+#define PT_LAYERED_FN_F __device__ __forceinline__
+#else
+#define PT_LAYERED_FN_F __device__ __noinline__
+#endif
+#if PT_LAYERED_SAMPLE_INLINE
+#define PT_LAYERED_FN_S __device__ __forceinline__
+#else
+#define PT_LAYERED_FN_S __device__ __noinline__
+#endif
+PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
     // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code).
     // The top interface is the rough or smooth dielectric, the bottom the Lambertian.  Terms
     // that depend on one direction only are computed once per direction (TRDir): wo and wi
@@ -665,7 +699,7 @@ __device__ __noinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness,
     return mk(fdiv(f.x, 5.0f), fdiv(f.y, 5.0f), fdiv(f.z, 5.0f));
 }
 
-__device__ __noinline__ bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+PT_LAYERED_FN_S bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
     // GlossyDiffuse.h:372-524
     const int mode = kRadiance;
     const float thickness = 0.01f;

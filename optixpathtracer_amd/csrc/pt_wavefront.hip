@@ -208,6 +208,10 @@ constexpr int shf_block(int mode) {
 #endif
 constexpr int kBlockShB = PT_SHB_BLOCK;
 
+#ifndef PT_NEE_LEAN
+#define PT_NEE_LEAN 1  // k_shade_nee keeps four values live across the walk
+#endif
+
 // Block-wide compaction: every thread of the block calls this (uniform control flow);
 // threads with pred get consecutive slots.  `lds` is kWavesSh + 1 ints of shared memory
 // private to this call site.
@@ -1098,6 +1102,36 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene 
     const Hit h = decode_hit(hv);
     SurfaceHit sf;
     reconstruct<TEX>(S, h, mk(c.x, c.y, c.z), sf);
+#if PT_NEE_LEAN
+    // only the path, the light index, |cos| and the squared distance stay live across the layered
+    // walk; the throughput and the light are loaded again after it (the same values and
+    // operations as below, so the same bits)
+    const int aux = W.aux[path];
+    const int li = aux >> 1;
+    uint32_t seed = __float_as_uint(W.beta[path].w);
+    f3 lds;
+    float d2;
+    {
+        const DevLight lt = L.lights[li];
+        const f3 lpos = mk(lt.px, lt.py, lt.pz);
+        lds = to_local(sf.fr, normalize(lpos - sf.pos));
+        const f3 dd = sf.pos - lpos;
+        d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
+    }
+    const float cosl = abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+    f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
+    f3 spectrum = f * cosl;
+    const float4 bv = W.beta[path];
+    const f3 beta = mk(bv.x, bv.y, bv.z);
+    if (!is_zero(spectrum)) {
+        const float P = L.n_lights == 1 ? 1.0f : 1.0f / (float)L.n_lights;
+        const DevLight lt = L.lights[li];
+        f3 Li = mk(lt.cr, lt.cg, lt.cb) / d2;
+        f3 add = ((beta * spectrum) * Li) / (P * 1.0f);
+        float4 l = W.L[path];
+        W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
+    }
+#else
     const float4 bv = W.beta[path];
     uint32_t seed = __float_as_uint(bv.w);
     const f3 beta = mk(bv.x, bv.y, bv.z);
@@ -1117,6 +1151,7 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene 
         float4 l = W.L[path];
         W.L[path] = make_float4(l.x + add.x, l.y + add.y, l.z + add.z, 0.0f);
     }
+#endif
     W.beta[path] = make_float4(bv.x, bv.y, bv.z, __uint_as_float(seed));  // f may draw
 }
 
