@@ -364,6 +364,17 @@ __device__ __forceinline__ void stqs(float4* p, float4 v) {
 #define PT_NEE_MODE 0
 #endif
 __device__ __forceinline__ float4 ldq_pair(const float4* p) { return PT_TRACE_NTQ ? ldqs(p) : *p; }
+// the same for k_extend and k_shadow_vis (PT_TRACE_NTQ_X)
+#ifndef PT_TRACE_NTQ_X
+#define PT_TRACE_NTQ_X 0  // configs 3 / 5 +0.1 / +0.3 %, Lambert -0.6 %: not kept
+#endif
+__device__ __forceinline__ float4 ldq_x(const float4* p) { return PT_TRACE_NTQ_X ? ldqs(p) : *p; }
+__device__ __forceinline__ void stq_x(float4* p, float4 v) {
+    if (PT_TRACE_NTQ_X)
+        stqs(p, v);
+    else
+        *p = v;
+}
 __device__ __forceinline__ void stq_pair(float4* p, float4 v) {
     if (PT_TRACE_NTQ)
         stqs(p, v);
@@ -525,7 +536,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_extend(DevScene 
     trace_slice<kRayClosest, STATS, TEX>(
         S, n_trace, ts, W,
         [&](int ri, TravState& st) {
-            const float4 a = ro[ri], c = rd[ri];
+            const float4 a = ldq_x(ro + ri), c = ldq_x(rd + ri);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, 100.0f);
             st.path = __float_as_int(a.w);
         },
@@ -533,7 +544,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_extend(DevScene 
             // copy k of a bounce-0 ray is path st.path + k * n_trace (queue 0 is in path order);
             // copies = 1: k_shade0_pixel reads the pixel's one record for all its frames
             for (int k = 0; k < copies; ++k)
-                W.hit[ri + (size_t)k * n_trace] = hit_record(st.h, st.path + k * n_trace);
+                stq_x(W.hit + ri + (size_t)k * n_trace, hit_record(st.h, st.path + k * n_trace));
         });
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n);        // path segments
@@ -982,7 +993,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(false)) void k_shadow_vis(Dev
     trace_slice<kRayAny, false, TEX>(
         S, n, ts, W,
         [&](int j, TravState& st) {
-            const float4 a = W.sh_o[j], c = W.sh_d[j];
+            const float4 a = ldq_x(W.sh_o + j), c = ldq_x(W.sh_d + j);
             trav_init(st, mk(a.x, a.y, a.z), mk(c.x, c.y, c.z), 0.0f, c.w);
             st.path = __float_as_int(a.w);
         },

@@ -1,4 +1,8 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > gpurun_out/r05w_gputest.log 2>&1; rc=$?; tail -3 gpurun_out/r05w_gputest.log; exit $rc
+T=r05x
+timeout -k 10 500 tools/ab.sh "old new" 3 --scene sphere_box_conductor --fpl 64 --spp 64 > gpurun_out/${T}_ab_ntx_c3.log 2>&1 || exit 1
+timeout -k 10 500 tools/ab.sh "old new" 3 --scene sponza_class --fpl 64 --spp 64 > gpurun_out/${T}_ab_ntx_c5.log 2>&1 || exit 1
+timeout -k 10 300 tools/ab.sh "old new" 2 --scene sphere_box_diffuse --fpl 64 --spp 64 --modes 1,3 > gpurun_out/${T}_ab_ntx_c2.log 2>&1 || exit 1
+for c in c3 c5 c2; do python3 tools/ab_summary.py gpurun_out/${T}_ab_ntx_$c.log; done
