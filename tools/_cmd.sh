@@ -1,5 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-( timeout -k 10 200 python3 tools/build_probe.py --soup 1000000 --builders 4,3,1,2 --repeat 2 &&
-  timeout -k 10 300 python3 tools/build_probe.py --soup 4000000 --builders 4,3,1 --repeat 2 ) > gpurun_out/r05y_build_soup.log 2>&1; rc=$?; grep -v amdgpu gpurun_out/r05y_build_soup.log; exit $rc
+T=r05zb
+timeout -k 10 700 tools/ab.sh "trd0 cur" 4 --scene sphere_box_dielectric20 --fpl 64 --spp 128 > gpurun_out/${T}_ab_trd_4d.log 2>&1 || exit 1
+timeout -k 10 700 tools/ab.sh "trd0 cur" 3 --scene sphere_box_layered --fpl 64 --spp 64 > gpurun_out/${T}_ab_trd_4l.log 2>&1 || exit 1
+python3 tools/ab_summary.py gpurun_out/${T}_ab_trd_4d.log; python3 tools/ab_summary.py gpurun_out/${T}_ab_trd_4l.log
