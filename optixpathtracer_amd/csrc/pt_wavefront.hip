@@ -144,9 +144,10 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
 // Default / Layered shading items are queued per bucket (shade_bucket): kShadeBuckets NEE and
 // kShadeBuckets BSDF-sample counters follow the two queue counters.
 constexpr int kShadeBuckets = 3;
-constexpr int kCnt = 2 + 2 * kShadeBuckets;
+constexpr int kCnt = 5 + 2 * kShadeBuckets;
 constexpr int kCntStride = 32;  // ints per counter = 128 B
-enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kShadeBuckets };
+// kPool*: the run-time ray pools of k_trace_pair, k_extend and k_shadow_vis (RayPool)
+enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kShadeBuckets, kPool = 2 + 2 * kShadeBuckets, kPoolExt, kPoolSh };
 __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
 // Path throughput | seed.  W.beta in path order (the phases of a bounce read it by path), except
 // in the Lambert mode: in queue order next to the ray, ping-pong like ray_o / ray_d (queue b
@@ -326,12 +327,39 @@ constexpr int kRefillMin = PT_REFILL_MIN;
                          // 20 / 24 / 32: -7 / -2 / -0.3 / 0 / -0.3 / -5 %)
 #endif
 
-__device__ __forceinline__ void wave_slice(int n, int& first, int& end) {
+// chunk_log = k > 0: the queue is cut into chunks of 2^k rays dealt round-robin to the waves,
+// so every wave's share samples the whole queue instead of one contiguous stretch of image rows
+// (whose cost differs from the next stretch's).  A wave then walks a virtual range [0, count) of
+// its chunks, and slice_ray maps a virtual index to the queue index.  k_extend and k_shadow_vis
+// use PT_SLICE_CHUNK_LOG_X, k_trace_pair contiguous slices.
+#ifndef PT_SLICE_CHUNK_LOG
+#define PT_SLICE_CHUNK_LOG 0
+#endif
+#ifndef PT_SLICE_CHUNK_LOG_X
+#define PT_SLICE_CHUNK_LOG_X PT_SLICE_CHUNK_LOG
+#endif
+__device__ __forceinline__ void wave_slice(int n, int& first, int& end, int chunk_log = 0) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
+    if (chunk_log > 0) {
+        const int K = 1 << chunk_log;
+        const int chunks = (n + K - 1) / K;
+        const int mine = chunks > wave ? (chunks - 1 - wave) / nwaves + 1 : 0;
+        first = 0;
+        // only the queue's last chunk is partial, and it is the last chunk of its wave
+        end = mine * K - ((chunks > 0 && (chunks - 1) % nwaves == wave) ? chunks * K - n : 0);
+        return;
+    }
     const int per = (n + nwaves - 1) / nwaves;
     first = min(n, wave * per);
     end = min(n, first + per);
+}
+// queue index of the wave's virtual index v (identity without chunks)
+__device__ __forceinline__ int slice_ray(int v, int chunk_log) {
+    if (chunk_log == 0) return v;
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
+    return (((v >> chunk_log) * nwaves + wave) << chunk_log) + (v & ((1 << chunk_log) - 1));
 }
 
 typedef float pt_v4f __attribute__((ext_vector_type(4)));
@@ -382,6 +410,43 @@ __device__ __forceinline__ void stq_pair(float4* p, float4 v) {
         *p = v;
 }
 
+// PT_TAIL_PROBE = 1 (measurement only): every k_trace_pair wave adds its start and end times
+// (s_memrealtime, 100 MHz) to module counters, and the last wave of the launch prints the launch
+// span, the waves' mean lifetime and the spread of their end times, so the static slices' tail
+// can be read off.
+#ifndef PT_TAIL_PROBE
+#define PT_TAIL_PROBE 0
+#endif
+#if PT_TAIL_PROBE
+__device__ unsigned long long g_tail[5];  // ~min start, max end, sum end, finished waves, sum start
+__device__ __forceinline__ void tail_probe_begin(unsigned long long& t0) {
+    t0 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&g_tail[0], ~t0);
+        atomicAdd(&g_tail[4], t0);
+    }
+}
+__device__ __forceinline__ void tail_probe_end(int b) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) != 0) return;
+    atomicMax(&g_tail[1], t1);
+    atomicAdd(&g_tail[2], t1);
+    __threadfence();
+    const unsigned long long nw = (unsigned long long)gridDim.x * (blockDim.x / 64);
+    if (atomicAdd(&g_tail[3], 1ull) == nw - 1) {
+        __threadfence();
+        const unsigned long long t0 = ~atomicAdd(&g_tail[0], 0ull), te = atomicAdd(&g_tail[1], 0ull);
+        const unsigned long long se = atomicAdd(&g_tail[2], 0ull), ss = atomicAdd(&g_tail[4], 0ull);
+        const double mean_end = (double)se / (double)nw - (double)t0, mean_start = (double)ss / (double)nw - (double)t0;
+        printf("TAIL b=%d waves=%llu span_us=%.1f mean_start_us=%.1f mean_end_us=%.1f idle_frac=%.4f\n", b, nw,
+               (double)(te - t0) / 100.0, mean_start / 100.0, mean_end / 100.0,
+               1.0 - (mean_end - mean_start) / (double)(te - t0));
+        for (int k = 0; k < 5; ++k) atomicExch(&g_tail[k], 0ull);  // vector atomics, no plain stores
+        __threadfence();
+    }
+}
+#endif
+
 // Lane-refilling trace loop over a queue slice: `fetch(ri, state)` initialises lane state
 // for ray ri, `finish(ri, state)` consumes a finished ray.  A finish that returns a token is
 // split in two: its loads are issued before the refill's record loads and `commit(token)` (its
@@ -390,6 +455,24 @@ __device__ __forceinline__ void stq_pair(float4* p, float4 v) {
 // (`done`) until enough lanes are idle; then the wave runs one batch block that finishes the
 // parked rays and refills the idle lanes with the next rays of the slice.  The triangle
 // batches take acceptable hits only (wave_tri_batch), so a finished ray's answer is final.
+// The rays of a trace launch dealt at run time (PT_TRACE_POOL): queue range [begin, end), handed
+// out in chunks of PT_POOL_CHUNK through the counter ctr (zeroed with the queue counters) to the
+// waves whose static slices ran out.
+#ifndef PT_TRACE_POOL
+#define PT_TRACE_POOL 60  // percent of k_trace_pair's rays in the pool (0: static slices only)
+#endif
+#ifndef PT_TRACE_POOL_X
+#define PT_TRACE_POOL_X 60  // the same for k_extend and k_shadow_vis
+#endif
+#ifndef PT_POOL_CHUNK
+#define PT_POOL_CHUNK 512
+#endif
+struct RayPool {
+    int* ctr = nullptr;
+    int begin = 0, end = 0;
+    int chunk_log = 0;  // the static slices' chunk interleave (wave_slice)
+};
+
 struct NoCommit {
     template <class T>
     __device__ void operator()(const T&) const {}
@@ -397,7 +480,7 @@ struct NoCommit {
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TriBatchLds* tri_lds,
                                             TravStats& ts, const WFState& W, Fetch fetch, Finish finish,
-                                            Commit commit = Commit{}) {
+                                            Commit commit = Commit{}, RayPool pool = RayPool{}) {
     using Tok = decltype(finish(0, *static_cast<const TravState*>(nullptr)));
     constexpr bool kSplit = !std::is_void_v<Tok>;
     using TokS = std::conditional_t<kSplit, Tok, int>;
@@ -414,14 +497,30 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
     // slice (it finishes the ones in flight), at the start and at every 16th batch block; one wave
     // in eight workgroups relays the host word at every 64th
     uint32_t npoll = 0;
-    if (W.cancel_seen && wf_cancel_poll(W, false)) end = next;
+    int* pctr = pool.ctr;
+    int vlog = pool.chunk_log;  // the static slice walks chunk-interleaved virtual indices
+    if (W.cancel_seen && wf_cancel_poll(W, false)) {
+        end = next;
+        pctr = nullptr;
+    }
     while (true) {
         // batch block once enough lanes idle (it costs the wave about as much as a step), and
         // at every step once the slice is drained
         if ((int)__popcll(__ballot(ri < 0 || done)) >= kRefillMin || next >= end) {
             if (W.cancel_seen && (++npoll & 15) == 0 &&
-                wf_cancel_poll(W, (npoll & 63) == 0 && (blockIdx.x & 7) == 0 && threadIdx.x == 0))
+                wf_cancel_poll(W, (npoll & 63) == 0 && (blockIdx.x & 7) == 0 && threadIdx.x == 0)) {
                 end = next;
+                pctr = nullptr;
+            }
+            if (pctr && next >= end) {  // static share drained: the next chunk of the pool
+                int base = 0;
+                if ((threadIdx.x & 63) == 0) base = atomicAdd(pctr, PT_POOL_CHUNK);
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+                vlog = 0;
+                next = min(pool.begin + base, pool.end);
+                end = min(next + PT_POOL_CHUNK, pool.end);
+                if (next >= pool.end) pctr = nullptr;
+            }
 #if PT_CYCLE_PROBE
             const uint64_t c0 = probe_clock();
 #else
@@ -440,7 +539,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
             const unsigned long long m = __ballot(ri < 0);
             const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             if (ri < 0 && next + pre < end) {
-                ri = next + pre;
+                ri = vlog ? slice_ray(next + pre, vlog) : next + pre;
                 fetch(ri, st);
                 if (STATS) ts.rays++;
                 done = S.ntri <= 0;  // empty scene: no BVH root, every ray misses
@@ -503,21 +602,30 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
 // BVH levels, the triangle batches), then the lane-refilling loop.
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_queue(DevScene S, int first, int end, TravStats& ts, const WFState& W, Fetch fetch,
-                                            Finish finish, Commit commit = Commit{}) {
+                                            Finish finish, Commit commit = Commit{}, RayPool pool = RayPool{}) {
     __shared__ int stack[kStack * kBlockTrace];
     __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
     __shared__ TriBatchLds tri_batch[kTriBatchWaves];
     stage_top_nodes<kLdsNodes>(S, top);
     trace_range<ANY, STATS, TEX>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, W, fetch,
-                                 finish, commit);
+                                 finish, commit, pool);
 }
 
 template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
 __device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats& ts, const WFState& W, Fetch fetch,
-                                            Finish finish) {
+                                            Finish finish, int* pool_ctr) {
     int next, end;
-    wave_slice(n, next, end);
-    trace_queue<ANY, STATS, TEX>(S, next, end, ts, W, fetch, finish);
+    RayPool pool;
+    pool.chunk_log = PT_SLICE_CHUNK_LOG_X;
+    pool.end = n;
+    if (PT_TRACE_POOL_X > 0) {
+        pool.ctr = pool_ctr;
+        pool.begin = n - (int)((long long)n * PT_TRACE_POOL_X / 100);
+    } else {
+        pool.begin = n;
+    }
+    wave_slice(pool.begin, next, end, pool.chunk_log);
+    trace_queue<ANY, STATS, TEX>(S, next, end, ts, W, fetch, finish, NoCommit{}, pool);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -545,7 +653,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_extend(DevScene 
             // copies = 1: k_shade0_pixel reads the pixel's one record for all its frames
             for (int k = 0; k < copies; ++k)
                 stq_x(W.hit + ri + (size_t)k * n_trace, hit_record(st.h, st.path + k * n_trace));
-        });
+        }, cnt(W, b, kPoolExt));
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n);        // path segments
         atomicAdd(&counters[6], (unsigned long long)n_trace);  // rays traced by the timed trace kernels
@@ -822,6 +930,10 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
 template <bool STATS, bool TEX>
 __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
+#if PT_TAIL_PROBE
+    unsigned long long tp0;
+    tail_probe_begin(tp0);
+#endif
     const int n_ext = *cnt(W, b + 1, kQueue);
     const int n_sh = *cnt(W, b, kShadowQ);
     const float4* ro = W.ray_o[(b + 1) & 1];
@@ -901,8 +1013,20 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
     // trace a single ray kind; a mixed-kind loop serves both (per-kind loops in one kernel and
     // per-wave shares of both kinds were slower).
     int first, end;
-    wave_slice(n_ext + n_sh, first, end);
-    trace_queue<kRayMixed, STATS, TEX>(S, first, end, ts, W, fetch, finish, commit);
+    const int n_all = n_ext + n_sh;
+    RayPool pool;
+    if (PT_TRACE_POOL > 0) {
+        pool.ctr = cnt(W, b, kPool);
+        pool.end = n_all;
+        pool.begin = n_all - (int)((long long)n_all * PT_TRACE_POOL / 100);
+    } else {
+        pool.begin = pool.end = n_all;
+    }
+    wave_slice(pool.begin, first, end);
+    trace_queue<kRayMixed, STATS, TEX>(S, first, end, ts, W, fetch, finish, commit, pool);
+#if PT_TAIL_PROBE
+    tail_probe_end(b);
+#endif
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
         atomicAdd(&counters[0], (unsigned long long)n_ext);           // path segments
         atomicAdd(&counters[5], (unsigned long long)n_sh);            // shadow rays
@@ -1000,7 +1124,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(false)) void k_shadow_vis(Dev
         [&](int j, const TravState& st) {
             const bool occluded = st.h.tri >= 0;
             W.vis[j] = table ? (occluded ? 0 : 1) : (occluded ? -1 : st.path);
-        });
+        }, cnt(W, b, kPoolSh));
 }
 
 // PT_NEE_MODE 2: the unoccluded shadow rays of k_trace_pair(b) add their contributions to the
