@@ -120,15 +120,16 @@ def parse():
                     help="samples per pixel per step: per GPU (weak configs) or in total (strong configs)")
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--kernel", type=int, default=2, help="0 = megakernel, 1 = wavefront, 2 = auto")
-    ap.add_argument("--frames-per-launch", type=int, default=64)
+    ap.add_argument("--frames-per-launch", type=int, default=128)
     ap.add_argument("--no-dedup-check", action="store_true",
                     help="skip the extra step timed with pt_set_primary_dedup(0)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
                     help="PMC traffic per launch measured by tools/profile.sh (optional)")
-    ap.add_argument("--wavefront-streams", type=int, default=2,
-                    help="streams the wavefront batches alternate between (pt_set_wavefront_streams)")
+    ap.add_argument("--wavefront-streams", type=int, default=0,
+                    help="streams the wavefront batches alternate between (pt_set_wavefront_streams; "
+                         "0 = the library's auto: one for Lambert, two otherwise)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="override the config's scaling (all configs: strong = the step's spp in total, split "
                          "over the ranks; weak = the step's spp per rank)")
@@ -201,6 +202,8 @@ def main():
     r = setup_renderer(scene, args.width, args.height, args.depth, device=local_rank, kernel=args.kernel)
     r.set_frames_per_launch(args.frames_per_launch)
     r.set_wavefront_streams(args.wavefront_streams)
+    # the streams the timed region runs on: 0 is the library's auto (one for Lambert, two otherwise)
+    eff_streams = args.wavefront_streams or (1 if scene.material_mode == 1 else 2)
     if args.kernel != 0:  # wavefront (auto resolves to it): time every k_extend launch
         r.set_kernel_timing(True)
     setup_s = time.perf_counter() - t0
@@ -305,13 +308,14 @@ def main():
     # share of k_trace_pair's shadow rays that found their light unoccluded (each adds its
     # contribution to the path radiance: NEE_ADD_BYTES more algorithmic bytes)
     unocc_share = trav["nee_unoccluded"] / trav["pair_kernel_shadow_rays"] if trav and trav["pair_kernel_shadow_rays"] else 0.0
-    # Transparency: the timed steps alternate the wavefront batches between two streams
-    # (pt_set_wavefront_streams, default 2), so a trace launch shares the GPU with the other
-    # batch's kernels and its event window is longer than its solo run.  One more step on a
-    # single stream gives the trace kernels' solo launch time (roofline.single_stream).
+    # Transparency: with two streams the timed steps alternate the wavefront batches between them
+    # (pt_set_wavefront_streams; auto takes two outside the Lambert mode), so a trace launch shares
+    # the GPU with the other batch's kernels and its event window is longer than its solo run.
+    # One more step on a single stream gives the trace kernels' solo launch time
+    # (roofline.single_stream); on one stream the timed region is that run.
     single = None
     s1_all_ms = None  # single-stream mean over all trace launches (vmem rate)
-    if args.kernel != 0 and not args.no_dedup_check and args.wavefront_streams > 1:
+    if args.kernel != 0 and not args.no_dedup_check and eff_streams > 1:
         r.set_wavefront_streams(1)
         r.stats_reset()
         if dist is not None:
@@ -414,6 +418,11 @@ def main():
             avg_launch_s = kernel_s / launches
             bytes_def = "396 B per segment + 12 B per sample"
         achieved = per_launch_bytes / avg_launch_s / 1e9
+        if single is None and eff_streams == 1 and fused and trace_line:
+            # one stream: the timed region is the solo run
+            single = {"value": round(value, 3), "kernel": dom, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                      "achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                      "launches": launches, "note": "the timed region runs on one stream"}
         # PMC figures come from separate rocprofv3 passes committed under profiles/ (tools/profile.sh,
         # tools/pmc.sh); each carries the kernel-source hash it was measured on.  Only figures of
         # these sources fill the contract fields; older ones are listed under pmc_stale.
@@ -519,6 +528,7 @@ def main():
                                   4: "layered"}.get(scene.material_mode, str(scene.material_mode)),
                 "kernel": {0: "megakernel", 1: "wavefront", 2: "auto (wavefront)"}[args.kernel],
                 "frames_per_launch": args.frames_per_launch,
+                "wavefront_streams": eff_streams,
                 "parallelism": f"spp-shard x{world}",
                 "lbvh_build_ms": round(bvh_ms, 3),
                 # pt_options.bvh_builder = PT_BVH_AUTO: the binned-SAH binary tree built on the GPU
@@ -552,7 +562,7 @@ def main():
                 # includes time it shares the GPU with the other stream's kernels (single_stream
                 # gives the same kernel alone)
                 "window": ("timed region, two wavefront streams (concurrent launch windows)"
-                           if args.wavefront_streams > 1 else "timed region, one stream"),
+                           if eff_streams > 1 else "timed region, one stream"),
                 "binding": binding,
                 "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
                 # SURVEY.md §8(d) whole-path figure: (segments*396 + samples*12) / render time
@@ -675,7 +685,7 @@ def main():
                 "sample": out["cpu_baseline"]["sample"].split(",")[0] + " (GPU render of the same frame ids)",
                 "gpu_batches": n_batches,
                 "gpu_frames_per_batch": fpl_check,
-                "gpu_streams": min(n_batches, args.wavefront_streams),
+                "gpu_streams": min(n_batches, eff_streams),
             }
         print(json.dumps(out), flush=True)
     r.close()

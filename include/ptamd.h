@@ -202,8 +202,9 @@ int pt_set_lights(pt_renderer* r, const pt_point_light* lights, int32_t count);
 int pt_set_max_bounces(pt_renderer* r, int32_t max_bounces);
 int pt_set_material_mode(pt_renderer* r, int32_t material_mode);
 int pt_set_kernel(pt_renderer* r, int32_t kernel);
-/* frames (spp) rendered per launch by pt_render_frames (default 64): the megakernel loops them in
-   registers; the wavefront keeps all of their paths in flight in one kernel chain. */
+/* frames (spp) rendered per launch by pt_render_frames (default 128 since round 5; 64 before): the
+   megakernel loops them in registers; the wavefront keeps all of their paths in flight in one
+   kernel chain, at most 2^28 paths (128 frames at 1080p, 56 GB of queues per stream). */
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames);
 /* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */
 int pt_set_traversal_stats(pt_renderer* r, int32_t enable);
@@ -215,10 +216,14 @@ int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
  * hit record to every frame (default 1).  0 traces every frame's copy; the images are
  * bit-identical either way. */
 int pt_set_primary_dedup(pt_renderer* r, int32_t enable);
-/* Wavefront: streams the batches of a pt_render_frames call alternate between (1 to 4, default
- * 2).  With more than 1, consecutive batches run on different streams with their own queues, so
- * one batch's kernels overlap another's; the batches still add into the sum in frame order, and
- * the image is bit-identical to 1.  A call uses at most as many streams as it has batches. */
+/* Wavefront: streams the batches of a pt_render_frames call alternate between (1 to 4, or 0 =
+ * auto, the default since round 5: one for the Lambert mode, two otherwise; a one-frame call in
+ * row bands takes two in every mode).  With more than 1, consecutive batches run on different
+ * streams with their own queues, so one batch's kernels overlap another's; the batches still add
+ * into the sum in frame order, and the image is bit-identical to 1.  A call uses at most as many
+ * streams as it has batches.  Round 5: with the trace kernels' ray pools a second
+ * stream no longer pays for Lambert (1537 vs 1508 Msamples/s at 128 frames) and still does for
+ * Dielectric (+4 %). */
 int pt_set_wavefront_streams(pt_renderer* r, int32_t streams);
 /* Wavefront, a call of one frame (pt_render without render-ahead, pt_render_frames with n = 1,
  * pt_launch): with 2 or more wavefront streams, the frame's rows are split into two bands that

@@ -105,7 +105,7 @@ struct pt_renderer {
     // wavefront batches alternate between two streams, each with its own queues, so one batch's
     // kernels overlap the other's (pt_set_wavefront_streams; 1 = everything on `stream`)
     static constexpr int kMaxWFStreams = 4;
-    int wf_streams = 2;
+    int wf_streams = 0;  // 0 = auto (launch_frames): one for Lambert, two otherwise
     hipStream_t xstream[kMaxWFStreams] = {};  // [0] unused: stream 0 is `stream`
     WFState xwf[kMaxWFStreams];               // [0] unused: stream 0's queues are `wf`
     hipEvent_t ev_fork = nullptr, ev_join[kMaxWFStreams] = {}, ev_accum[2] = {nullptr, nullptr};
@@ -229,7 +229,8 @@ struct pt_renderer {
     double last_ms = 0.0, total_ms = 0.0;
     uint64_t calls = 0;
     double bvh_ms = 0.0;
-    int frames_per_launch = 64;  // 28 GB of queues at 1080p (16 -> 64 frames +5 % Lambert)
+    int frames_per_launch = 128;  // 56 GB of queues at 1080p (16 -> 64 frames +5 % Lambert,
+                                  // 64 -> 128 with the ray pools +0.7 to +2.5 %)
     // multi-device (pt_options.n_devices >= 1): this renderer is device 0 of the list; peers are
     // single-device renderers of the other devices; comms[g] is device g's RCCL communicator
     std::vector<pt_renderer*> peers;
@@ -368,7 +369,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // each band's kernels fill the other's SIMT tails.  Every pixel's path depends only on its
         // pixel and frame id, so the image is the same bit for bit.
         const bool bands = n == 1 && r->band_split && r->height >= 16;  // both bands non-empty
-        int ns = std::max(1, std::min(r->wf_streams, bands ? 2 : nbatch));
+        const int want = r->wf_streams > 0 ? r->wf_streams : (bands || r->material_mode != PT_MAT_LAMBERT ? 2 : 1);
+        int ns = std::max(1, std::min(want, bands ? 2 : nbatch));
         for (int k = 0; k < ns; ++k) {
             WFState& w = k ? r->xwf[k] : r->wf;
             if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces) {
@@ -1761,8 +1763,8 @@ extern "C" int pt_set_traversal_stats(pt_renderer* r, int32_t enable) {
 }
 
 extern "C" int pt_set_wavefront_streams(pt_renderer* r, int32_t streams) {
-    if (!r || streams < 1 || streams > pt_renderer::kMaxWFStreams)
-        return fail(PT_ERR_INVALID, "pt_set_wavefront_streams: 1 to 4");
+    if (!r || streams < 0 || streams > pt_renderer::kMaxWFStreams)
+        return fail(PT_ERR_INVALID, "pt_set_wavefront_streams: 0 (auto) or 1 to 4");
     int rc = collect_pending(r);
     if (rc != PT_OK) return rc;
     r->wf_streams = streams;

@@ -356,16 +356,17 @@ def test_shallow_depth_and_light_count(depth, mode, n_lights):
 
 @pytest.mark.parametrize("mode", [1, 3, 0])
 def test_wavefront_two_streams_bit_identical(mode):
-    """pt_set_wavefront_streams(2) (the default) alternates the batches of a call between two
-    streams with their own queues; k_accum still adds the batches in frame order, so the sum --
-    fp32 and fp64 -- equals the one-stream sum bit for bit, also across calls and with the
-    trace-kernel timing on (11 frames = batches of 4 + 4 + 3)."""
+    """pt_set_wavefront_streams(2) (the auto default's choice outside the Lambert mode) alternates
+    the batches of a call between two streams with their own queues; k_accum still adds the
+    batches in frame order, so the sum -- fp32 and fp64 -- equals the one-stream sum bit for bit,
+    also across calls and with the trace-kernel timing on (11 frames = batches of 4 + 4 + 3).
+    0 (auto) gives the same image."""
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import setup_renderer
 
     sc = scenes.tiny_scene("conductor" if mode == 0 else "diffuse")
     out = {}
-    for streams in (1, 2, 3):
+    for streams in (1, 2, 3, 0):
         for fp64 in (False, True):
             r = setup_renderer(sc, 48, 40, 5, kernel=1)
             r.set_material_mode(mode)
@@ -380,7 +381,7 @@ def test_wavefront_two_streams_bit_identical(mode):
             out[streams, fp64] = (r.accum(), r.stats())
             r.close()
     for fp64 in (False, True):
-        for streams in (2, 3):
+        for streams in (2, 3, 0):
             (a, sa), (b, sb) = out[1, fp64], out[streams, fp64]
             np.testing.assert_array_equal(a, b)
             assert sa["segments"] == sb["segments"]
@@ -388,7 +389,7 @@ def test_wavefront_two_streams_bit_identical(mode):
     from optixpathtracer_amd.capi import PTError
 
     r = setup_renderer(sc, 16, 16, 2, kernel=1)
-    for bad in (0, 5, -1):  # 1 to 4 streams
+    for bad in (5, -1):  # 0 (auto) or 1 to 4 streams
         with pytest.raises(PTError):
             r.set_wavefront_streams(bad)
     r.close()
