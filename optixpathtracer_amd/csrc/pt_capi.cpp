@@ -231,6 +231,8 @@ struct pt_renderer {
     double bvh_ms = 0.0;
     int frames_per_launch = 128;  // 56 GB of queues at 1080p (16 -> 64 frames +5 % Lambert,
                                   // 64 -> 128 with the ray pools +0.7 to +2.5 %)
+    int nf_fit = 0;  // > 0: the largest batch whose queues fitted after an out-of-memory halving
+                     // (launch_frames); cleared by pt_set_frames_per_launch and pt_resize
     // multi-device (pt_options.n_devices >= 1): this renderer is device 0 of the list; peers are
     // single-device renderers of the other devices; comms[g] is device g's RCCL communicator
     std::vector<pt_renderer*> peers;
@@ -357,8 +359,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // Lambert 1080p 545 / 648 / 664 Msamples/s at 1 / 8 / 16 frames.
         constexpr int kMaxWFPaths = 1 << 28;  // 56 GB of queues at 208 B per path
         const int P = r->width * r->height;
-        const int nf_cap = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
-                                                 kMaxWFPaths / std::max(1, P)}));
+        int nf_cap = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
+                                           kMaxWFPaths / std::max(1, P), r->nf_fit > 0 ? r->nf_fit : (1 << 30)}));
         // two batches or more: alternate them between two streams with their own queues, so one
         // batch's kernels run beside the other's (the memory-bound shading of one beside the
         // VALU-bound tracing of the other, and each kernel's SIMT tail filled); k_accum still adds
@@ -377,7 +379,15 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                 for (int j = 0; j < pt_renderer::kMaxWFStreams; ++j)
                     if (r->wf_stream(j)) PT_HIP(hipStreamSynchronize(r->wf_stream(j)), "hipStreamSynchronize");
                 wavefront_free(w);
-                const hipError_t ae = wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces));
+                hipError_t ae = wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces));
+                // the first stream's queues: halve the batch until they fit (every batch size gives
+                // the same image), PT_ERR_NOMEM only when one frame does not; the size that fitted
+                // stays the cap until pt_set_frames_per_launch or pt_resize
+                while (ae == hipErrorOutOfMemory && k == 0 && nf_cap > 1) {
+                    nf_cap = (nf_cap + 1) / 2;
+                    r->nf_fit = nf_cap;
+                    ae = wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces));
+                }
                 // the extra streams only overlap batches: when their queues do not fit, render on
                 // the k streams that do (the image is the same, added in frame order either way)
                 if (ae == hipErrorOutOfMemory && k > 0) {
@@ -1142,6 +1152,7 @@ int pt_resize(pt_renderer* r, int32_t width, int32_t height) {
     // unsized renderer, on which the render calls return PT_ERR_STATE)
     r->width = r->height = 0;
     r->user_accum = nullptr;
+    r->nf_fit = 0;  // a new size: the queues may fit the full batch again
     PT_HIP(hipMalloc(&r->d_frame, bytes), "hipMalloc frame");
     PT_HIP(hipMalloc(&r->d_accum, bytes), "hipMalloc accum");
     PT_HIP(hipMemsetAsync(r->d_accum, 0, bytes, r->stream), "hipMemset accum");
@@ -1590,7 +1601,11 @@ int pt_set_render_ahead_budget(pt_renderer* r, float max_ms) {
 int pt_set_frames_per_launch(pt_renderer* r, int32_t frames) {
     if (!r || frames < 1) return fail(PT_ERR_INVALID, "pt_set_frames_per_launch: invalid");
     r->frames_per_launch = frames;
-    for (pt_renderer* p : r->peers) p->frames_per_launch = frames;
+    r->nf_fit = 0;
+    for (pt_renderer* p : r->peers) {
+        p->frames_per_launch = frames;
+        p->nf_fit = 0;
+    }
     return PT_OK;
 }
 

@@ -1,13 +1,14 @@
 """Device out-of-memory behaviour of the wavefront queues.
 
-A batch's queues hold 208 B per path: 28 GB at 1920x1080 with 64 frames per batch, one queue set
-per wavefront stream.  The tests take most of the card's free memory with a hipMalloc first
+A batch's queues hold 208 B per path: 56 GB at 1920x1080 with 128 frames per batch (the
+default), one queue set per wavefront stream.  The tests take most of the card's free memory with a hipMalloc first
 (through the HIP runtime libptamd.so links: torch ships a second HIP runtime, which finds no GPU
 once ours holds the device in the same process), so the queues cannot all be allocated:
 
 * when an extra stream's queues do not fit, the call renders on the streams that do (same image);
-* when the first stream's queues do not fit, the call fails with PT_ERR_NOMEM and leaves no
-  partial queue set behind, so lowering frames-per-launch and calling again renders correctly.
+* when the first stream's queues do not fit, the call halves its batch until they do (the same
+  image); only when one frame's queues do not fit does it fail with PT_ERR_NOMEM, leaving no
+  partial queue set behind, so the same renderer renders once the memory is back.
 """
 import numpy as np
 import pytest
@@ -51,9 +52,13 @@ def test_queue_allocation_failures_fall_back_and_retry():
     sc = scenes.make_scene("sphere_box_diffuse")
     ref, sr = gpu_render(sc, W, H, DEPTH, 1, FRAMES, streams=1)
     per_stream = QUEUE_BYTES_PER_PATH * W * H * 64
+    per_frame = QUEUE_BYTES_PER_PATH * W * H
 
-    # room for one queue set and a half: the second stream's allocation fails -> one stream
+    # 64-frame batches on two streams, room for one queue set and a half: the second stream's
+    # allocation fails -> one stream
     r = setup_renderer(sc, W, H, DEPTH)
+    r.set_frames_per_launch(64)
+    r.set_wavefront_streams(2)
     blk = _Block(1.5 * per_stream)
     r.accum_clear()
     r.render_frames(1, FRAMES)
@@ -61,21 +66,27 @@ def test_queue_allocation_failures_fall_back_and_retry():
     blk.release()
     r.close()
 
-    # room for half a queue set: PT_ERR_NOMEM, then a retry with smaller batches succeeds
+    # the default batch (128 frames) with room for half a 64-frame queue set: the call halves its
+    # batch until the first stream's queues fit (32 or 16 frames) and renders the same image
     r = setup_renderer(sc, W, H, DEPTH)
     blk = _Block(0.5 * per_stream)
-    r.accum_clear()
-    with pytest.raises(PTError) as ei:
-        r.render_frames(1, FRAMES)
-    assert ei.value.status == PT_ERR_NOMEM
-    r.set_frames_per_launch(8)  # 3.5 GB per stream
     r.accum_clear()
     r.render_frames(1, FRAMES)
     np.testing.assert_array_equal(r.accum(), ref)
     assert r.stats()["samples"] == W * H * FRAMES
     blk.release()
-    # and with the memory back, the original batch size works on the same renderer
-    r.set_frames_per_launch(64)
+    r.close()
+
+    # room for half of one frame's queues: PT_ERR_NOMEM with no partial queue set left behind,
+    # and with the memory back the same renderer renders the full batch
+    r = setup_renderer(sc, W, H, DEPTH)
+    blk = _Block(0.5 * per_frame)
+    r.accum_clear()
+    with pytest.raises(PTError) as ei:
+        r.render_frames(1, FRAMES)
+    assert ei.value.status == PT_ERR_NOMEM
+    blk.release()
+    r.set_frames_per_launch(128)  # clears the cap the halving left
     r.accum_clear()
     r.render_frames(1, FRAMES)
     np.testing.assert_array_equal(r.accum(), ref)
