@@ -19,7 +19,7 @@ spp per step); the driver's default run is configs[1].
 
 Extra fields: `roofline` (HBM roofline of the mode's dominant kernel, measured with one HIP event
 pair per launch on the stream it runs on, per kernel: in the Lambert / Conductor / Dielectric modes
-k_trace_pair (the shadow rays of bounce b and the extension rays of b+1 of a 64-frame batch), 48
+k_trace_pair (the shadow rays of bounce b and the extension rays of b+1 of a batch of --frames-per-launch frames, 128 by default), 48
 algorithmic bytes per traced ray (an extension ray's 32-B record read and 16-B hit record written,
 a shadow ray's three 16-B records read) plus 32 B (radiance read and write) per unoccluded shadow
 ray, whose share comes from the untimed traversal-statistics render; in the Default / Layered modes
@@ -294,7 +294,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         e3 = float(t.item())
         value_other = (other, args.width * args.height * (args.spp * world if other == "weak" else args.spp) / e3 / 1e6)
-    # One more untimed render of two 64-frame batches with the traversal counters on (a separate
+    # One more untimed render of two batches with the traversal counters on (a separate
     # kernel instance): node visits (global / from LDS), triangle tests and rays per trace launch,
     # for the vector-memory roofline of the trace kernels (roofline.vmem).  Its time is not used.
     trav = None
@@ -397,7 +397,7 @@ def main():
             per_launch_bytes = trace_line["bytes_per_launch"]
             avg_launch_s = trace_line["avg_launch_ms"] / 1e3
             bytes_def = ("48 B per traced ray of one k_trace_pair launch (the shadow rays of bounce b and the "
-                         "extension rays of bounce b+1 of a 64-frame batch): an extension ray's 32-B record read "
+                         "extension rays of bounce b+1 of one batch): an extension ray's 32-B record read "
                          "and 16-B hit record written, a shadow ray's direction, contribution and origin records "
                          f"read; plus {NEE_ADD_BYTES} B (radiance read + write) per unoccluded shadow ray "
                          f"({unocc_share:.4f} of the shadow rays, traversal-statistics render)")

@@ -27,11 +27,11 @@ else
   echo "[round] profile"
   timeout -k 10 900 tools/profile.sh $TAG > "$OUT/profile.log" 2>&1
   tail -3 "$OUT/profile.log"
-  echo "[round] pmc (SQ / TCC / TCP passes, Lambert, 64 frames)"
-  timeout -k 10 600 tools/pmc.sh gpurun_out/pmc_$TAG --fpl 64 --spp 64 > "$OUT/pmc.log" 2>&1
+  echo "[round] pmc (SQ / TCC / TCP passes, Lambert, 128 frames)"
+  timeout -k 10 600 tools/pmc.sh gpurun_out/pmc_$TAG --fpl 128 --spp 128 > "$OUT/pmc.log" 2>&1
   tail -1 "$OUT/pmc.log"
-  echo "[round] pmc (TA / TD / TCP passes, Lambert, 64 frames)"
-  timeout -k 10 600 tools/pmc_ta.sh gpurun_out/pmcta_$TAG --fpl 64 --spp 64 > "$OUT/pmc_ta.log" 2>&1
+  echo "[round] pmc (TA / TD / TCP passes, Lambert, 128 frames)"
+  timeout -k 10 600 tools/pmc_ta.sh gpurun_out/pmcta_$TAG --fpl 128 --spp 128 > "$OUT/pmc_ta.log" 2>&1
   tail -1 "$OUT/pmc_ta.log"
   # VALU issue of k_shade_nee, the dominant kernel of the Default / Layered configs (bench.py
   # roofline.valu reads profiles/shade_valu_config<C>.json): one SQ pass per config
@@ -40,10 +40,10 @@ else
     cfg=${c%%:*}; sc=${c#*:}
     echo "[round] shade VALU pass, config $cfg"
     timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU \
-      --output-format csv -d "$OUT/shv_$cfg" -o run -- python3 tools/perf_probe.py --scene $sc --fpl 64 --spp 64 --repeat 1 \
+      --output-format csv -d "$OUT/shv_$cfg" -o run -- python3 tools/perf_probe.py --scene $sc --fpl 128 --spp 128 --repeat 1 \
       > "$OUT/shv_$cfg.log" 2>&1
     python3 tools/pmc_summary.py "$OUT/shv_$cfg" k_shade_nee --shade-json "$OUT/shade_valu_config$cfg.json" \
-      --source "tools/round.sh $TAG profile (rocprofv3 SQ pass, perf_probe --scene $sc --fpl 64 --spp 64)" | tail -3
+      --source "tools/round.sh $TAG profile (rocprofv3 SQ pass, perf_probe --scene $sc --fpl 128 --spp 128)" | tail -3
   done
   # kernel stats of the Default-mode configs' own bench command
   for cfg in 3 5; do
