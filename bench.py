@@ -129,7 +129,7 @@ def parse():
                     help="PMC traffic per launch measured by tools/profile.sh (optional)")
     ap.add_argument("--wavefront-streams", type=int, default=0,
                     help="streams the wavefront batches alternate between (pt_set_wavefront_streams; "
-                         "0 = the library's auto: one for Lambert, two otherwise)")
+                         "0 = the library's auto: two for Conductor and Dielectric, one otherwise)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="override the config's scaling (all configs: strong = the step's spp in total, split "
                          "over the ranks; weak = the step's spp per rank)")
@@ -203,7 +203,7 @@ def main():
     r.set_frames_per_launch(args.frames_per_launch)
     r.set_wavefront_streams(args.wavefront_streams)
     # the streams the timed region runs on: 0 is the library's auto (one for Lambert, two otherwise)
-    eff_streams = args.wavefront_streams or (1 if scene.material_mode == 1 else 2)
+    eff_streams = args.wavefront_streams or (2 if scene.material_mode in (2, 3) else 1)
     if args.kernel != 0:  # wavefront (auto resolves to it): time every k_extend launch
         r.set_kernel_timing(True)
     setup_s = time.perf_counter() - t0
@@ -309,7 +309,7 @@ def main():
     # contribution to the path radiance: NEE_ADD_BYTES more algorithmic bytes)
     unocc_share = trav["nee_unoccluded"] / trav["pair_kernel_shadow_rays"] if trav and trav["pair_kernel_shadow_rays"] else 0.0
     # Transparency: with two streams the timed steps alternate the wavefront batches between them
-    # (pt_set_wavefront_streams; auto takes two outside the Lambert mode), so a trace launch shares
+    # (pt_set_wavefront_streams; auto takes two for Conductor and Dielectric), so a launch shares
     # the GPU with the other batch's kernels and its event window is longer than its solo run.
     # One more step on a single stream gives the trace kernels' solo launch time
     # (roofline.single_stream); on one stream the timed region is that run.

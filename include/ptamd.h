@@ -217,13 +217,13 @@ int pt_set_kernel_timing(pt_renderer* r, int32_t enable);
  * bit-identical either way. */
 int pt_set_primary_dedup(pt_renderer* r, int32_t enable);
 /* Wavefront: streams the batches of a pt_render_frames call alternate between (1 to 4, or 0 =
- * auto, the default since round 5: one for the Lambert mode, two otherwise; a one-frame call in
- * row bands takes two in every mode).  With more than 1, consecutive batches run on different
+ * auto, the default since round 5: two for the Conductor and Dielectric modes, one otherwise; a
+ * one-frame call in row bands takes two in every mode).  With more than 1, consecutive batches run on different
  * streams with their own queues, so one batch's kernels overlap another's; the batches still add
  * into the sum in frame order, and the image is bit-identical to 1.  A call uses at most as many
  * streams as it has batches.  Round 5: with the trace kernels' ray pools a second
- * stream no longer pays for Lambert (1537 vs 1508 Msamples/s at 128 frames) and still does for
- * Dielectric (+4 %). */
+ * stream no longer pays for Lambert (1537 vs 1508 Msamples/s at 128 frames), Default or Layered,
+ * and still does for Dielectric (+4 %) and Conductor (+0.6 %). */
 int pt_set_wavefront_streams(pt_renderer* r, int32_t streams);
 /* Wavefront, a call of one frame (pt_render without render-ahead, pt_render_frames with n = 1,
  * pt_launch): with 2 or more wavefront streams, the frame's rows are split into two bands that

@@ -356,7 +356,7 @@ def test_shallow_depth_and_light_count(depth, mode, n_lights):
 
 @pytest.mark.parametrize("mode", [1, 3, 0])
 def test_wavefront_two_streams_bit_identical(mode):
-    """pt_set_wavefront_streams(2) (the auto default's choice outside the Lambert mode) alternates
+    """pt_set_wavefront_streams(2) (the auto default's choice for Conductor and Dielectric) alternates
     the batches of a call between two streams with their own queues; k_accum still adds the
     batches in frame order, so the sum -- fp32 and fp64 -- equals the one-stream sum bit for bit,
     also across calls and with the trace-kernel timing on (11 frames = batches of 4 + 4 + 3).
