@@ -467,6 +467,15 @@ __device__ __forceinline__ void tail_probe_end(int b) {
 #ifndef PT_POOL_CHUNK
 #define PT_POOL_CHUNK 512
 #endif
+// launches of fewer rays than this many per wave keep static slices only: a one-frame call's
+// launches (about 300 rays per wave) ran 40 % slower with the pool
+#ifndef PT_POOL_MIN_PER_WAVE
+#define PT_POOL_MIN_PER_WAVE 2048
+#endif
+__device__ __forceinline__ bool pool_pays(int n) {
+    const long long nwaves = (long long)((gridDim.x * blockDim.x) >> 6);
+    return (long long)n >= nwaves * PT_POOL_MIN_PER_WAVE;
+}
 struct RayPool {
     int* ctr = nullptr;
     int begin = 0, end = 0;
@@ -618,7 +627,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats&
     RayPool pool;
     pool.chunk_log = PT_SLICE_CHUNK_LOG_X;
     pool.end = n;
-    if (PT_TRACE_POOL_X > 0) {
+    if (PT_TRACE_POOL_X > 0 && pool_pays(n)) {
         pool.ctr = pool_ctr;
         pool.begin = n - (int)((long long)n * PT_TRACE_POOL_X / 100);
     } else {
@@ -1015,7 +1024,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
     int first, end;
     const int n_all = n_ext + n_sh;
     RayPool pool;
-    if (PT_TRACE_POOL > 0) {
+    if (PT_TRACE_POOL > 0 && pool_pays(n_all)) {
         pool.ctr = cnt(W, b, kPool);
         pool.end = n_all;
         pool.begin = n_all - (int)((long long)n_all * PT_TRACE_POOL / 100);
