@@ -207,6 +207,9 @@ constexpr int shf_block(int mode) {
 #ifndef PT_SHB_WAVES
 #define PT_SHB_WAVES 4  // waves per SIMD the register allocator must allow (128 VGPRs)
 #endif
+#ifndef PT_SMP_WAVES
+#define PT_SMP_WAVES 5  // k_shade_smp: 96 VGPRs, 4-12 spilled; configs 3 / 5 / Layered +0.6 / +0.5 / +0.9 % over 4
+#endif
 constexpr int kBlockShB = PT_SHB_BLOCK;
 
 #ifndef PT_NEE_LEAN
@@ -1302,7 +1305,7 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene 
 // BSDF sample + continuation of a Default / Layered bounce (devicePrograms.cu:474-509) over the
 // bucketed sample queue; continuation rays are appended to queue b + 1.
 template <int MODE, bool TEX>
-__global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_smp(DevScene S, DevLaunch L, WFState W, int b) {
+__global__ __launch_bounds__(kBlockShB, PT_SMP_WAVES) void k_shade_smp(DevScene S, DevLaunch L, WFState W, int b) {
     constexpr int kW = kBlockShB / 64;
     __shared__ int lds_q[kW + 1];
     if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kSmp0)) return;  // block-uniform

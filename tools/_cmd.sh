@@ -1,9 +1,8 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-T=r05zu
-for v in m0 m2k m0 m2k; do
-  PTAMD_LIB=optixpathtracer_amd/_variants/lib_$v.so timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --reference-loops 512 > gpurun_out/${T}_$v.json 2> gpurun_out/${T}_$v.log || exit 1
-  python3 -c "
-import json;d=json.load(open('gpurun_out/${T}_$v.json'));rl=d['reference_loop'];print('$v', d['value'], d['value_reference_loop'], rl['first_call_after_change_ms'], rl['no_render_ahead'])"
-done
+T=r05zw
+timeout -k 10 500 tools/ab.sh "base smp5" 3 --scene sphere_box_conductor --fpl 128 --spp 128 > gpurun_out/${T}_ab_smp5_c3.log 2>&1 || exit 1
+timeout -k 10 500 tools/ab.sh "base smp5" 2 --scene sponza_class --fpl 128 --spp 128 > gpurun_out/${T}_ab_smp5_c5.log 2>&1 || exit 1
+timeout -k 10 500 tools/ab.sh "base smp5" 2 --scene sphere_box_layered --fpl 128 --spp 128 > gpurun_out/${T}_ab_smp5_4l.log 2>&1 || exit 1
+for c in c3 c5 4l; do python3 tools/ab_summary.py gpurun_out/${T}_ab_smp5_$c.log; done
