@@ -138,6 +138,11 @@ class pt_stats(C.Structure):
         ("pair_kernel_bytes", C.c_uint64),
         ("pair_kernel_shadow_rays", C.c_uint64),
         ("nee_unoccluded", C.c_uint64),
+        ("queue_bytes", C.c_uint64),
+        ("queue_budget", C.c_uint64),
+        ("last_streams", C.c_int32),
+        ("last_batch_frames", C.c_int32),
+        ("look_ahead_held", C.c_uint64),
     ]
 
 
@@ -177,6 +182,8 @@ SIGNATURES = {
     "pt_set_frames_per_launch": (C.c_int, [_R, C.c_int32]),
     "pt_set_render_ahead": (C.c_int, [_R, C.c_int32]),
     "pt_set_render_ahead_budget": (C.c_int, [_R, C.c_float]),
+    "pt_set_queue_budget": (C.c_int, [_R, C.c_int64]),
+    "pt_set_debug_hold": (C.c_int, [_R, C.c_int32]),
     "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel_timing": (C.c_int, [_R, C.c_int32]),
     "pt_render": (C.c_int, [_R, _FP]),

@@ -172,6 +172,9 @@ struct pt_renderer {
         hipEvent_t start = nullptr, ready = nullptr;  // recorded on `stream` around the slot's batch
         bool measured = true;                         // its duration is in frame_ms_est
         bool speculative = false;                     // a cancellable look-ahead batch (cancel_look_ahead)
+        // a speculative batch a call has taken a frame from (render_frame_image): no longer
+        // cancellable, and a cancel of a later batch waits for it first
+        bool served = false;
     };
     RingSlot ring[2];
     int ring_k = 1, ring_last = 0;  // ramp length, slot rendered last
@@ -224,6 +227,12 @@ struct pt_renderer {
     unsigned* d_cancel_seen = nullptr;
     unsigned cancel_epoch = 0;
     uint64_t ahead_cancelled = 0;  // look-ahead batches cancelled (pt_stats)
+    // pt_set_debug_hold (tests): the next speculative batches start with k_hold, which waits until
+    // the batch is cancelled, the pinned release word is set, or 10 s pass
+    bool debug_hold = false;
+    unsigned* h_hold_release = nullptr;
+    unsigned* d_hold_release = nullptr;
+    uint64_t ahead_held = 0;  // speculative batches enqueued behind a hold (pt_stats)
     bool pending = false;
     uint64_t samples = 0;
     double last_ms = 0.0, total_ms = 0.0;
@@ -232,7 +241,12 @@ struct pt_renderer {
     int frames_per_launch = 128;  // 56 GB of queues at 1080p (16 -> 64 frames +5 % Lambert,
                                   // 64 -> 128 with the ray pools +0.7 to +2.5 %)
     int nf_fit = 0;  // > 0: the largest batch whose queues fitted after an out-of-memory halving
-                     // (launch_frames); cleared by pt_set_frames_per_launch and pt_resize
+                     // (launch_frames); cleared by pt_set_frames_per_launch and pt_resize, and once
+                     // the free memory would hold the full batch again
+    // pt_set_queue_budget: the most bytes all wavefront streams' queues may hold together
+    // (0 = default, a quarter of the device memory; < 0 = no budget, only the 2^28-path cap)
+    int64_t queue_budget = 0;
+    int last_streams = 0, last_batch = 0;  // streams and frames per batch of the last wavefront call
     // multi-device (pt_options.n_devices >= 1): this renderer is device 0 of the list; peers are
     // single-device renderers of the other devices; comms[g] is device g's RCCL communicator
     std::vector<pt_renderer*> peers;
@@ -324,6 +338,30 @@ DevLaunch make_launch(const pt_renderer* r, float* accum, uint32_t frame_base, u
     return L;
 }
 
+// Bytes the wavefront queues of all streams hold now.
+size_t queue_bytes_held(const pt_renderer* r) {
+    size_t b = r->wf.paths > 0 ? wavefront_bytes(r->wf.paths, r->wf.max_bounces) : 0;
+    for (int k = 1; k < pt_renderer::kMaxWFStreams; ++k)
+        if (r->xwf[k].paths > 0) b += wavefront_bytes(r->xwf[k].paths, r->xwf[k].max_bounces);
+    return b;
+}
+
+// The most bytes all streams' queues may hold together (pt_set_queue_budget): the caller's
+// figure, or by default a quarter of the device memory -- 72 GB on an MI355X, above the 56 GB the
+// 128-frame 1080p batch takes on one stream, so the Lambert, Default and Layered modes keep it,
+// while two-stream Conductor / Dielectric calls take 82-frame batches.  SIZE_MAX:
+// no budget.
+size_t queue_budget_bytes(const pt_renderer* r) {
+    if (r->queue_budget < 0) return SIZE_MAX;
+    if (r->queue_budget > 0) return (size_t)r->queue_budget;
+    size_t total = 0;
+    if (hipDeviceTotalMem(&total, r->device) != hipSuccess || total == 0) {
+        (void)hipGetLastError();
+        return SIZE_MAX;
+    }
+    return total / 4;
+}
+
 // Launch frames [first, first+n) in chunks, adding into accum; brackets with events.  Does not
 // wait for earlier work: the event pairs of every launch since the last synchronisation point
 // are summed at the next pt_synchronize / pt_get_stats / download (collect_pending).
@@ -359,8 +397,20 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         // Lambert 1080p 545 / 648 / 664 Msamples/s at 1 / 8 / 16 frames.
         constexpr int kMaxWFPaths = 1 << 28;  // 56 GB of queues at 208 B per path
         const int P = r->width * r->height;
-        int nf_cap = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
-                                           kMaxWFPaths / std::max(1, P), r->nf_fit > 0 ? r->nf_fit : (1 << 30)}));
+        const int maxb = std::max(1, r->max_bounces);
+        const int nf_full = std::max(1, std::min({r->frames_per_launch, (int)std::min<uint32_t>(n, 1u << 20),
+                                                  kMaxWFPaths / std::max(1, P)}));
+        // a batch size that fitted after an out-of-memory halving is kept until the free memory
+        // (plus what the queues hold now) would take the full batch again
+        if (r->nf_fit > 0 && r->nf_fit < nf_full) {
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+                if (free_b + queue_bytes_held(r) >= wavefront_bytes(P * nf_full, maxb)) r->nf_fit = 0;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
+        int nf_cap = std::min(nf_full, r->nf_fit > 0 ? r->nf_fit : (1 << 30));
         // two batches or more: alternate them between two streams with their own queues, so one
         // batch's kernels run beside the other's (the memory-bound shading of one beside the
         // VALU-bound tracing of the other, and each kernel's SIMT tail filled); k_accum still adds
@@ -377,20 +427,54 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         const bool two = r->material_mode == PT_MAT_CONDUCTOR || r->material_mode == PT_MAT_DIELECTRIC;
         const int want = r->wf_streams > 0 ? r->wf_streams : (bands || two ? 2 : 1);
         int ns = std::max(1, std::min(want, bands ? 2 : nbatch));
+        // the queue budget (pt_set_queue_budget): the ns streams' queues
+        // together stay within it, by smaller batches (every batch size gives the same image);
+        // queues that streams beyond ns still hold are freed when they would overrun it
+        const size_t budget = queue_budget_bytes(r);
+        if (budget != SIZE_MAX) {
+            const size_t per_frame = wavefront_bytes(P, maxb);
+            const int nf_b = (int)std::max<size_t>(1, budget / ((size_t)ns * per_frame));
+            nf_cap = std::min(nf_cap, nf_b);
+            size_t used = (size_t)ns * wavefront_bytes(P * nf_cap, maxb);
+            for (int k = ns; k < pt_renderer::kMaxWFStreams; ++k) {
+                if (r->xwf[k].paths == 0) continue;
+                const size_t held = wavefront_bytes(r->xwf[k].paths, r->xwf[k].max_bounces);
+                if (used + held <= budget) {
+                    used += held;
+                    continue;
+                }
+                PT_HIP(hipStreamSynchronize(r->xstream[k]), "hipStreamSynchronize");
+                wavefront_free(r->xwf[k]);
+            }
+        }
         for (int k = 0; k < ns; ++k) {
             WFState& w = k ? r->xwf[k] : r->wf;
-            if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces) {
+            // queues larger than the budget's share (a lowered budget) are allocated again, smaller
+            const bool over = budget != SIZE_MAX && w.paths > 0 && (size_t)ns * wavefront_bytes(w.paths, w.max_bounces) > budget;
+            if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces || over) {
                 for (int j = 0; j < pt_renderer::kMaxWFStreams; ++j)
                     if (r->wf_stream(j)) PT_HIP(hipStreamSynchronize(r->wf_stream(j)), "hipStreamSynchronize");
                 wavefront_free(w);
-                hipError_t ae = wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces));
+                hipError_t ae = wavefront_alloc(w, P * nf_cap, maxb);
+                if (ae == hipErrorOutOfMemory && k == 0) {
+                    // queues of the other streams (an earlier call's, or a mode with more
+                    // streams) go first, then the full batch again
+                    bool freed = false;
+                    for (int j = 1; j < pt_renderer::kMaxWFStreams; ++j)
+                        if (r->xwf[j].paths > 0) {
+                            wavefront_free(r->xwf[j]);
+                            freed = true;
+                        }
+                    if (freed) ae = wavefront_alloc(w, P * nf_cap, maxb);
+                }
                 // the first stream's queues: halve the batch until they fit (every batch size gives
                 // the same image), PT_ERR_NOMEM only when one frame does not; the size that fitted
-                // stays the cap until pt_set_frames_per_launch or pt_resize
+                // stays the cap until the memory would take the full batch (above),
+                // pt_set_frames_per_launch or pt_resize
                 while (ae == hipErrorOutOfMemory && k == 0 && nf_cap > 1) {
                     nf_cap = (nf_cap + 1) / 2;
                     r->nf_fit = nf_cap;
-                    ae = wavefront_alloc(w, P * nf_cap, std::max(1, r->max_bounces));
+                    ae = wavefront_alloc(w, P * nf_cap, maxb);
                 }
                 // the extra streams only overlap batches: when their queues do not fit, render on
                 // the k streams that do (the image is the same, added in frame order either way)
@@ -401,6 +485,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                 PT_HIP(ae, "wavefront_alloc");
             }
         }
+        r->last_streams = ns;
+        r->last_batch = nf_cap;
         const bool dual = ns > 1;
         if (dual && !r->ev_fork) {
             PT_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming), "hipEventCreate");
@@ -467,6 +553,10 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                 wq.cancel_host = r->d_cancel_host;
                 wq.cancel_seen = r->d_cancel_seen;
                 wq.cancel_epoch = r->cancel_epoch;
+                if (r->debug_hold && r->d_hold_release && batch == 0) {  // pt_set_debug_hold: k_hold first
+                    wq.hold_release = r->d_hold_release;
+                    r->ahead_held++;
+                }
             }
             PT_HIP(launch_wavefront_frame(r->material_mode, r->trav_stats, S, L, wq, first + f,
                                           nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
@@ -540,6 +630,7 @@ void ring_free(pt_renderer* r) {
         s.n = 0;
         s.measured = true;
         s.speculative = false;
+        s.served = false;
     }
     r->ring_k = 1;
     r->ahead_oom_cap = 1 << 30;
@@ -634,6 +725,7 @@ int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t f
     pt_renderer::RingSlot& sl = r->ring[s];
     sl.n = 0;
     sl.measured = true;
+    sl.served = false;
     sl.speculative = speculative && cancel_words(r);
     int rc = ring_reserve(r, s, std::max(n, cap), n3);
     if (rc == PT_OK) PT_HIP(hipEventRecord(sl.start, r->stream), "hipEventRecord");
@@ -660,10 +752,17 @@ int ring_fill(pt_renderer* r, int s, const pt_renderer::RenderKey& k, uint32_t f
 void cancel_look_ahead(pt_renderer* r, bool force = false) {
     if (!r->spec_pending || !r->h_cancel) return;
     pt_renderer::RingSlot& sl = r->ring[r->ring_last];
-    if (sl.n == 0 || !sl.speculative) return;
+    if (sl.n == 0 || !sl.speculative) return;  // not speculative: also a batch a call took a frame from
     if (!force && sl.key == render_key(r)) return;
     if (hipEventQuery(sl.ready) == hipSuccess) return;  // done: its frames stay valid for their state
     (void)hipGetLastError();                            // hipErrorNotReady
+    // The epoch stops every batch enqueued under an older one: a served batch still in flight
+    // (the other slot, enqueued earlier on the same stream) finishes first
+    pt_renderer::RingSlot& other = r->ring[r->ring_last ^ 1];
+    if (other.served && other.n > 0 && hipEventQuery(other.ready) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipEventSynchronize(other.ready);
+    }
     ++r->cancel_epoch;
     __atomic_store_n(r->h_cancel, r->cancel_epoch, __ATOMIC_SEQ_CST);
     sl.n = 0;
@@ -720,7 +819,14 @@ int render_frame_image(pt_renderer* r, const float** img, hipEvent_t* ready = nu
             }
         }
         if (rc == PT_OK) {
-            const pt_renderer::RingSlot& sl = r->ring[s];
+            pt_renderer::RingSlot& sl = r->ring[s];
+            // A frame handed out of a speculative batch may be read by work the caller has
+            // already queued behind it (pt_display_add_frame's blend does not wait for the
+            // batch): the batch is no longer cancellable
+            if (sl.speculative) {
+                sl.speculative = false;
+                sl.served = true;
+            }
             *img = sl.d + (size_t)(f - sl.first) * n3;
             if (ready) *ready = sl.ready;
             r->ahead_served++;
@@ -1084,6 +1190,7 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
 
 int pt_destroy(pt_renderer* r) {
     if (!r) return PT_OK;
+    if (r->h_hold_release) __atomic_store_n(r->h_hold_release, 1u, __ATOMIC_SEQ_CST);  // a held batch ends now
     for (pt_renderer* p : r->peers) (void)hipSetDevice(p->device), (void)hipStreamSynchronize(p->stream);
     (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
@@ -1111,6 +1218,7 @@ int pt_destroy(pt_renderer* r) {
     if (r->d_debug) (void)hipFree(r->d_debug);
     if (r->d_cancel_seen) (void)hipFree(r->d_cancel_seen);
     if (r->h_cancel) (void)hipHostFree(r->h_cancel);
+    if (r->h_hold_release) (void)hipHostFree(r->h_hold_release);
     wavefront_free(r->wf);
     for (int k = 1; k < pt_renderer::kMaxWFStreams; ++k) {
         wavefront_free(r->xwf[k]);
@@ -1536,6 +1644,12 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
     out->pair_kernel_bytes = c[17];
     out->pair_kernel_shadow_rays = c[19];
     out->nee_unoccluded = c[18];
+    out->queue_bytes = queue_bytes_held(r);
+    const size_t qb = queue_budget_bytes(r);
+    out->queue_budget = qb == SIZE_MAX ? 0 : qb;
+    out->last_streams = r->last_streams;
+    out->last_batch_frames = r->last_batch;
+    out->look_ahead_held = r->ahead_held;
     // a multi-device renderer reports the work of all its devices (times are device 0's)
     for (pt_renderer* p : r->peers) {
         pt_stats ps;
@@ -1559,6 +1673,11 @@ int pt_get_stats(pt_renderer* r, pt_stats* out) {
         out->trace_kernel_bytes += ps.trace_kernel_bytes;
         out->strict_retraces += ps.strict_retraces;
         out->nee_unoccluded += ps.nee_unoccluded;
+        // the per-kernel ray and byte counts of every device, like trace_kernel_*
+        out->pair_kernel_rays += ps.pair_kernel_rays;
+        out->pair_kernel_bytes += ps.pair_kernel_bytes;
+        out->pair_kernel_shadow_rays += ps.pair_kernel_shadow_rays;
+        out->queue_bytes += ps.queue_bytes;
     }
     return PT_OK;
 }
@@ -1584,6 +1703,7 @@ int pt_stats_reset(pt_renderer* r) {
     r->shade_launches = 0;
     r->ahead_rendered = r->ahead_served = 0;
     r->ahead_cancelled = 0;
+    r->ahead_held = 0;
     return PT_OK;
 }
 
@@ -1610,6 +1730,36 @@ int pt_set_frames_per_launch(pt_renderer* r, int32_t frames) {
         p->frames_per_launch = frames;
         p->nf_fit = 0;
     }
+    return PT_OK;
+}
+
+int pt_set_queue_budget(pt_renderer* r, int64_t bytes) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_queue_budget: NULL");
+    r->queue_budget = bytes;
+    for (pt_renderer* p : r->peers) p->queue_budget = bytes;
+    return PT_OK;
+}
+
+int pt_set_debug_hold(pt_renderer* r, int32_t on) {
+    if (!r) return fail(PT_ERR_INVALID, "pt_set_debug_hold: NULL");
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
+    if (!r->h_hold_release) {
+        unsigned* h = nullptr;
+        void* d = nullptr;
+        PT_HIP(hipHostMalloc((void**)&h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent),
+               "hipHostMalloc hold word");
+        *h = 1u;
+        const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return hip_fail(e, "hipHostGetDevicePointer hold word");
+        }
+        r->h_hold_release = h;
+        r->d_hold_release = static_cast<unsigned*>(d);
+    }
+    // on: later speculative batches wait in k_hold; off: a batch waiting there goes on now
+    __atomic_store_n(r->h_hold_release, on ? 0u : 1u, __ATOMIC_SEQ_CST);
+    r->debug_hold = on != 0;
     return PT_OK;
 }
 

@@ -44,7 +44,11 @@ __device__ __forceinline__ float div_short(float a, float b) {
     // mismatch in 2^34 random pairs without this).  Those lanes take the compiler's last step.
     // (Expected false, so the compiler keeps it a branch instead of computing both steps on
     // every lane; no asm barrier, which would also stop it from merging equal divisions.)
-    if (__builtin_expect(scale, 0)) q = __builtin_amdgcn_div_fmasf(__builtin_fmaf(-d, q, n), y, q, true);
+#ifndef PT_DIV_PROBE_NOBRANCH
+#define PT_DIV_PROBE_NOBRANCH 0  // timing probe only (wrong on rescaled quotients): the branch's cost
+#endif
+    if (!PT_DIV_PROBE_NOBRANCH && __builtin_expect(scale, 0))
+        q = __builtin_amdgcn_div_fmasf(__builtin_fmaf(-d, q, n), y, q, true);
     return __builtin_amdgcn_div_fixupf(q, b, a);
 }
 

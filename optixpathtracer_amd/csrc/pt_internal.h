@@ -85,6 +85,9 @@ struct WFState {
     const unsigned* cancel_host = nullptr;  // pinned host word: the newest cancel epoch (PCIe reads)
     unsigned* cancel_seen = nullptr;        // device relay of it (agent-scope loads, L2-served)
     unsigned cancel_epoch = 0;
+    // pt_set_debug_hold (tests only): a speculative batch with this pinned word starts with k_hold,
+    // which returns once the batch is cancelled, the word is set, or 10 s have passed
+    const unsigned* hold_release = nullptr;
 };
 size_t wavefront_bytes(int paths, int max_bounces);
 // sum32[i] = (float)sum64[i] (the multi-device fp64 reduce's result -> the fp32 sum buffer)

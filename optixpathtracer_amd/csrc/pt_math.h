@@ -51,11 +51,27 @@ struct f3 {
 };
 
 PT_HD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+// PT_PK_F3 = 1: on the device the x and y channels of the f3 products and sums go through
+// two-wide vectors, which gfx950 executes as v_pk_mul_f32 / v_pk_add_f32 (IEEE per element, so
+// every result is the same bits as the scalar operations).
+#ifndef PT_PK_F3
+#define PT_PK_F3 0
+#endif
+#if PT_PK_F3 && defined(__HIP_DEVICE_COMPILE__)
+typedef float pk2 __attribute__((ext_vector_type(2)));
+PT_HD pk2 lo2(f3 a) { return pk2{a.x, a.y}; }
+PT_HD f3 operator+(f3 a, f3 b) { const pk2 v = lo2(a) + lo2(b); return mk(v.x, v.y, a.z + b.z); }
+PT_HD f3 operator-(f3 a, f3 b) { const pk2 v = lo2(a) - lo2(b); return mk(v.x, v.y, a.z - b.z); }
+PT_HD f3 operator*(f3 a, f3 b) { const pk2 v = lo2(a) * lo2(b); return mk(v.x, v.y, a.z * b.z); }
+PT_HD f3 operator*(f3 a, float s) { const pk2 v = lo2(a) * pk2{s, s}; return mk(v.x, v.y, a.z * s); }
+PT_HD f3 operator*(float s, f3 a) { const pk2 v = pk2{s, s} * lo2(a); return mk(v.x, v.y, s * a.z); }
+#else
 PT_HD f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 PT_HD f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 PT_HD f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 PT_HD f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 PT_HD f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+#endif
 PT_HD f3 operator/(f3 a, float s) { return mk(fdiv(a.x, s), fdiv(a.y, s), fdiv(a.z, s)); }
 PT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 PT_HD bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }

@@ -19,16 +19,18 @@ namespace {
 
 struct Box {
     float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    // bounds take -0 as +0 (x + 0 under round-to-nearest), as the GPU builder's ordered-int
+    // atomics do (pt_sah_gpu.hip f2o): the two builders' boxes agree in the sign of zero
     void grow(const Box& b) {
         for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], b.lo[a]);
-            hi[a] = std::max(hi[a], b.hi[a]);
+            lo[a] = std::min(lo[a], b.lo[a] + 0.0f);
+            hi[a] = std::max(hi[a], b.hi[a] + 0.0f);
         }
     }
     void grow(const float p[3]) {
         for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], p[a]);
-            hi[a] = std::max(hi[a], p[a]);
+            lo[a] = std::min(lo[a], p[a] + 0.0f);
+            hi[a] = std::max(hi[a], p[a] + 0.0f);
         }
     }
     float half_area() const {

@@ -45,15 +45,19 @@ constexpr int kSmallWaves = kSmallBlock / 64;
 constexpr int kSmallStack = 16;  // > log2(kSmallMax): the larger child is stacked, the smaller one goes on
 
 // Order-preserving int encoding of a (non-NaN) float, for atomic min / max.
+// -0 is taken as +0 first (f + 0 under round-to-nearest): the ordered encoding puts -0 below +0,
+// where the host's std::min / std::max keep whichever zero came first; both
+// builders now see only +0, so their boxes agree in the sign of zero as well.
 __device__ __forceinline__ int f2o(float f) {
-    const int i = __float_as_int(f);
+    const int i = __float_as_int(f + 0.0f);
     return i >= 0 ? i : i ^ 0x7fffffff;
 }
 __device__ __forceinline__ float o2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 
 // pt_sah.cpp Box::grow (std::min / std::max: a NaN operand never replaces the bound)
-__device__ __forceinline__ float gmin_h(float a, float p) { return p < a ? p : a; }
-__device__ __forceinline__ float gmax_h(float a, float p) { return a < p ? p : a; }
+// (-0 taken as +0, as Box::grow does since round 6)
+__device__ __forceinline__ float gmin_h(float a, float p) { p += 0.0f; return p < a ? p : a; }
+__device__ __forceinline__ float gmax_h(float a, float p) { p += 0.0f; return a < p ? p : a; }
 
 // pt_sah.cpp Box::half_area
 __device__ __forceinline__ float box_half_area(float lx, float ly, float lz, float hx, float hy, float hz) {

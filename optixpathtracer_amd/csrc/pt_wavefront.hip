@@ -100,6 +100,27 @@ __device__ __forceinline__ bool wf_cancelled(const WFState& W) {
     return wf_cancel_poll(W, (blockIdx.x & 63) == 0 && threadIdx.x == 0);
 }
 
+// pt_set_debug_hold (tests only): the first kernel of a held speculative
+// batch.  One lane waits until the host cancels the batch (a newer epoch in the pinned cancel
+// word, relayed into cancel_seen as wf_cancel_poll does), releases the hold (the pinned release
+// word), or 10 s of the 100-MHz wall clock pass, with an iteration bound behind that.  Every later
+// kernel of the batch is queued behind it, so a test can move the camera while the batch is
+// provably in flight, whatever the speed of the GPU.
+__global__ void k_hold(WFState W) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const unsigned long long t0 = wall_clock64();
+    for (int it = 0; it < (1 << 22); ++it) {
+        const unsigned h = __hip_atomic_load(W.cancel_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (h > W.cancel_epoch) {
+            __hip_atomic_fetch_max(W.cancel_seen, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (__hip_atomic_load(W.hold_release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+        if (wall_clock64() - t0 > 1000000000ull) return;
+        __builtin_amdgcn_s_sleep(64);
+    }
+}
+
 // Hit record of a finished extension ray: (path, u, v, tri | back << 31), or a miss.  The
 // shading kernels reconstruct the surface from (tri, u, v) and never read t, so the first word
 // carries the path id and they skip the ray_o read.
@@ -1542,7 +1563,12 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
                                   hipEvent_t accum_done, const hipEvent_t* shade_events, int* n_shade_timed) {
     const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
-    hipError_t e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
+    hipError_t e = hipSuccess;
+    if (W.cancel_seen && W.hold_release) {  // pt_set_debug_hold: the batch waits in k_hold first
+        hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, stream, W);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    e = hipMemsetAsync(W.count, 0, count_bytes(maxb), stream);
     if (e != hipSuccess) return e;
     // fused modes with the primary dedup: frame 0's camera rays only (k_camera `lean`, shade0)
     const bool lean = fused_mode(mode) && primary_dedup && nf > 1 && maxb > 0;

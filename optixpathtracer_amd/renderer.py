@@ -179,6 +179,15 @@ class OptixRenderer:
     def set_frames_per_launch(self, frames: int) -> None:
         check(self.lib.pt_set_frames_per_launch(self.h, int(frames)), "pt_set_frames_per_launch")
 
+    def set_queue_budget(self, nbytes: int) -> None:
+        """pt_set_queue_budget: bytes for all streams' wavefront queues (0 = default, a quarter of the
+        device memory; < 0 = none)."""
+        check(self.lib.pt_set_queue_budget(self.h, int(nbytes)), "pt_set_queue_budget")
+
+    def set_debug_hold(self, on: bool) -> None:
+        """pt_set_debug_hold (tests): speculative look-ahead batches wait until cancelled or released."""
+        check(self.lib.pt_set_debug_hold(self.h, 1 if on else 0), "pt_set_debug_hold")
+
     def set_traversal_stats(self, enable: bool) -> None:
         check(self.lib.pt_set_traversal_stats(self.h, 1 if enable else 0), "pt_set_traversal_stats")
 

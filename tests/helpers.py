@@ -16,7 +16,9 @@ def image_mse(a: np.ndarray, b: np.ndarray) -> float:
 def gpu_render(scene, width, height, max_bounces, first_frame, n_frames, mode=None, kernel=2, device=0,
                frames_per_launch=None, streams=None, kernel_timing=False):
     """Render through the C ABI.  kernel 2 (PT_KERNEL_AUTO, the default) is the product path
-    bench.py times: the wavefront with 64-frame batches alternating over two streams."""
+    bench.py times: the wavefront with the library's default batches (128 frames, within the queue
+    budget) on auto streams (two for Conductor / Dielectric, one otherwise), unless
+    frames_per_launch / streams override them."""
     from optixpathtracer_amd.renderer import setup_renderer
 
     r = setup_renderer(scene, width, height, max_bounces, device=device, kernel=kernel)

@@ -91,3 +91,72 @@ def test_queue_allocation_failures_fall_back_and_retry():
     r.render_frames(1, FRAMES)
     np.testing.assert_array_equal(r.accum(), ref)
     r.close()
+
+
+def test_queue_budget_bounds_the_batch():
+    """pt_set_queue_budget bounds the queues of all streams together.  The
+    default (a quarter of the device memory) keeps the 128-frame 1080p batch of one stream; a
+    smaller budget lowers the frames per batch (the same image); -1 lifts it."""
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    sc = scenes.make_scene("sphere_box_diffuse")
+    ref, _ = gpu_render(sc, W, H, DEPTH, 1, FRAMES, streams=1)
+    P = W * H
+    r = setup_renderer(sc, W, H, DEPTH)
+    r.accum_clear()
+    r.render_frames(1, FRAMES)
+    st = r.stats()
+    assert st["queue_budget"] > 0 and st["queue_bytes"] <= st["queue_budget"]
+    assert st["last_streams"] == 1 and st["last_batch_frames"] == 128
+    np.testing.assert_array_equal(r.accum(), ref)
+    for streams, frames in ((1, 20), (2, 20), (2, 7)):
+        budget = frames * QUEUE_BYTES_PER_PATH * P + (1 << 20)  # room for the counters
+        r.set_queue_budget(budget)
+        r.set_wavefront_streams(streams)
+        r.accum_clear()
+        r.render_frames(1, FRAMES)
+        st = r.stats()
+        assert st["queue_budget"] == budget
+        assert st["queue_bytes"] <= budget, (streams, frames, st["queue_bytes"])
+        assert st["last_streams"] == streams
+        assert st["last_batch_frames"] == max(1, frames // streams), (streams, frames, st["last_batch_frames"])
+        np.testing.assert_array_equal(r.accum(), ref)
+    r.set_queue_budget(-1)  # none: the full batch on both streams
+    r.accum_clear()
+    r.render_frames(1, FRAMES)
+    st = r.stats()
+    assert st["queue_budget"] == 0 and st["last_batch_frames"] == 128 and st["last_streams"] == 2
+    np.testing.assert_array_equal(r.accum(), ref)
+    r.close()
+
+
+def test_out_of_memory_frees_idle_stream_queues_first():
+    """queues held by streams a call does not use (an earlier two-stream Conductor
+    call's) are freed before the first stream's batch is halved, so a renderer does not stay on
+    small batches because of memory it holds itself."""
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.capi import PT_MAT_CONDUCTOR, PT_MAT_LAMBERT
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    sc = scenes.make_scene("sphere_box_diffuse")
+    ref, _ = gpu_render(sc, W, H, DEPTH, 1, FRAMES, streams=1)
+    per_stream = QUEUE_BYTES_PER_PATH * W * H * 64
+    r = setup_renderer(sc, W, H, DEPTH)
+    r.set_queue_budget(-1)  # this test is about the out-of-memory path, not the budget
+    r.set_material_mode(PT_MAT_CONDUCTOR)
+    r.set_frames_per_launch(64)
+    r.accum_clear()
+    r.render_frames(1, FRAMES)
+    st = r.stats()
+    assert st["last_streams"] == 2 and st["queue_bytes"] >= 2 * per_stream
+    blk = _Block(0.2 * per_stream)  # free: a fifth of a 64-frame set; held: two of them
+    r.set_material_mode(PT_MAT_LAMBERT)  # one stream, 128 frames: needs both sets' memory
+    r.set_frames_per_launch(128)
+    r.accum_clear()
+    r.render_frames(1, FRAMES)
+    st = r.stats()
+    assert st["last_streams"] == 1 and st["last_batch_frames"] == 128
+    np.testing.assert_array_equal(r.accum(), ref)
+    blk.release()
+    r.close()

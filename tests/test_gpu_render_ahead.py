@@ -198,18 +198,20 @@ def test_render_ahead_debug_pixel():
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["default", "lambert"])
 def test_look_ahead_cancelled_by_camera_move(mode):
-    """a camera move while the look-ahead batch is in flight cancels it
-    (pt_capi.cpp cancel_look_ahead; its kernels stop at their next poll, pt_wavefront.hip
-    wf_cancel_poll), and the next call's frame is the fresh render of the new camera, bit for bit.
-    With no time budget the ramp is 1, 2, ..., 64 frames, so call 64 is served from the first
-    64-frame slot and enqueues the next 64 frames on speculation (tens of ms of GPU work at this
-    size); the move follows that call at once, with the batch in flight.  The renderer without
+    """a camera move while the look-ahead batch is in
+    flight cancels it (pt_capi.cpp cancel_look_ahead; its kernels stop at their next poll,
+    pt_wavefront.hip wf_cancel_poll), and the next call's frame is the fresh render of the new
+    camera, bit for bit.  With no time budget the ramp is 1, 2, ..., 64 frames, so call 64 is
+    served from the first 64-frame slot and enqueues the next 64 frames on speculation.  The
+    debug hold (pt_set_debug_hold) makes that batch wait in k_hold until it is cancelled, so the
+    move provably finds it in flight, whatever the GPU's speed (round 5 sized the image so the
+    batch would still be running, and a fast box finished it first).  The renderer without
     render-ahead replays the same calls afterwards for the bit-for-bit comparison."""
     from optixpathtracer_amd import scenes
     from optixpathtracer_amd.renderer import setup_renderer
 
     sc = scenes.sphere_in_box("conductor")
-    w, h, depth = 960, 540, 8
+    w, h, depth = 320, 180, 8
     shape = (h, w, 3)
     a = setup_renderer(sc, w, h, depth)
     b = setup_renderer(sc, w, h, depth)
@@ -217,11 +219,15 @@ def test_look_ahead_cancelled_by_camera_move(mode):
     for r in (a, b):
         r.set_material_mode(mode)
     a.set_render_ahead_budget(0)  # no time bound: the ramp reaches 64 frames
+    a.set_debug_hold(True)
     pos = np.asarray(sc.camera_blender_pos, np.float32) + np.float32(0.02)
     fa = [a.Render(np.empty(shape, np.float32)).copy() for _ in range(64)]
-    a.SetCameraBlender(pos, sc.camera_blender_rot, sc.fov_deg)  # the look-ahead batch is in flight
+    a.SetCameraBlender(pos, sc.camera_blender_rot, sc.fov_deg)  # the look-ahead batch waits in k_hold
     fa += [a.Render(np.empty(shape, np.float32)).copy() for _ in range(2)]
-    assert a.stats()["look_ahead_cancelled"] == 1
+    st = a.stats()
+    assert st["look_ahead_held"] == 1
+    assert st["look_ahead_cancelled"] == 1
+    a.set_debug_hold(False)
     for k in range(66):
         if k == 64:
             b.SetCameraBlender(pos, sc.camera_blender_rot, sc.fov_deg)
@@ -243,4 +249,43 @@ def test_look_ahead_cancelled_by_camera_move(mode):
         r.SetLights(lights)
     _same_calls(a, b, 10, shape=shape)
     for r in (a, b, c):
+        r.close()
+
+
+def test_served_look_ahead_frame_survives_camera_move():
+    """pt_display_add_frame can take its frame from the speculative batch that
+    pt_render enqueued, and queues the blend behind it without waiting.  A camera move after that
+    must not cancel the batch (the blend would mix a partly rendered frame into the view): a batch
+    a call has taken a frame from is no longer cancellable.  The hold keeps the batch in flight
+    across the move; the progressive view must equal the one of a renderer without render-ahead."""
+    from optixpathtracer_amd import scenes
+    from optixpathtracer_amd.renderer import setup_renderer
+
+    sc = scenes.sphere_in_box("conductor")
+    w, h, depth = 320, 180, 8
+    shape = (h, w, 3)
+    a = setup_renderer(sc, w, h, depth)
+    b = setup_renderer(sc, w, h, depth)
+    b.set_render_ahead(1)
+    a.set_render_ahead_budget(0)
+    a.set_debug_hold(True)
+    for r in (a, b):
+        r.set_material_mode(1)
+        r.display_reset(-1)
+    _same_calls(a, b, 64, shape=shape)  # call 64 enqueues frames 65..128 on speculation (held)
+    for r in (a, b):
+        r.display_add_frame()  # frame 65: a takes it from the held batch
+    pos = np.asarray(sc.camera_blender_pos, np.float32) + np.float32(0.02)
+    for r in (a, b):
+        r.SetCameraBlender(pos, sc.camera_blender_rot, sc.fov_deg)
+    a.set_debug_hold(False)
+    np.testing.assert_array_equal(a.display(), b.display())
+    st = a.stats()
+    assert st["look_ahead_held"] == 1 and st["look_ahead_cancelled"] == 0
+    # both go on under the new camera
+    for r in (a, b):
+        r.display_add_frame()
+    np.testing.assert_array_equal(a.display(), b.display())
+    _same_calls(a, b, 3, shape=shape)
+    for r in (a, b):
         r.close()

@@ -101,3 +101,21 @@ def test_default_builder_is_gpu_sah():
     n1, t1, _ = _bvh(sc, SAH)
     np.testing.assert_array_equal(n0, n1)
     np.testing.assert_array_equal(t0, t1)
+
+
+def test_signed_zero_coordinates_identical():
+    """the GPU builder merges boxes with ordered-int atomics (-0 below +0) where the
+    host's std::min / std::max keep the first zero seen; both now take -0 as +0, so a mesh whose
+    coordinates mix -0 and +0 gives the same BVH4 bit for bit."""
+    rng = np.random.default_rng(11)
+    g = np.stack(np.meshgrid(np.arange(24), np.arange(24), indexing="ij"), -1).reshape(-1, 2).astype(np.float32)
+    grid = np.zeros((len(g), 3, 3), np.float32)
+    grid[:, :, :2] = g[:, None, :] - np.float32(12)
+    grid[:, 1, 0] += 1
+    grid[:, 2, 1] += 1
+    # z = +0 or -0 per vertex, and some x / y coordinates at -0 as well
+    grid[:, :, 2] = np.where(rng.random((len(g), 3)) < 0.5, np.float32(-0.0), np.float32(0.0))
+    zx = grid[:, :, 0] == 0
+    grid[:, :, 0][zx] = np.where(rng.random(int(zx.sum())) < 0.5, np.float32(-0.0), np.float32(0.0))
+    assert np.signbit(grid).any()
+    _same_bvh(_soup(grid))
