@@ -79,7 +79,13 @@ CONFIGS = {
            "BASELINE configs[3] (ii): Layered 1920x1080, 4096 spp split over the GPUs + RCCL reduce"),
     "5": ("sponza_class", 1024, "strong",
           "BASELINE configs[4]: Sponza-class procedural atrium (~250k tris, mixed BRDFs) 1920x1080, 1024 spp"),
+    "5t": ("sponza_textured", 1024, "strong",
+           "BASELINE configs[4], textured: the atrium with albedo / normal / metal-rough maps and alpha-cut-out "
+           "foliage (~250k tris, mixed BRDFs) 1920x1080, 1024 spp"),
 }
+# configs whose scene enters the renderer the way the reference's models do: written as .glb and
+# read by the C++ glTF loader (pt_model_load_gltf, ModelLoader::LoadModel's counterpart)
+GLB_CONFIGS = ("5", "5t")
 
 
 def log(*a):
@@ -112,7 +118,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
-                    help="BASELINE.json config: 2 = configs[1] (default, the headline), 3, 4d, 4l, 5")
+                    help="BASELINE.json config: 2 = configs[1] (default, the headline), 3, 4d, 4l, 5, 5t")
+    ap.add_argument("--scene-source", choices=["auto", "procedural", "glb"], default="auto",
+                    help="auto: configs 5 / 5t through a .glb and the C++ glTF loader, the others in memory")
     ap.add_argument("--scene", default=None, help="override the config's scene")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -198,6 +206,22 @@ def main():
     from optixpathtracer_amd.renderer import setup_renderer
 
     scene = scenes.make_scene(args.scene)
+    source = {"kind": "procedural (in memory)"}
+    if args.scene_source == "glb" or (args.scene_source == "auto" and args.config in GLB_CONFIGS):
+        # the reference's scenes enter through ModelLoader::LoadModel (ModelLoader.cpp:11-43): the
+        # procedural scene is written as one .glb (untimed) and read back by pt_model_load_gltf
+        import shutil
+        import tempfile
+
+        from optixpathtracer_amd import gltf
+
+        tmp = tempfile.mkdtemp(prefix="ptamd_glb_")
+        try:
+            scene, load_ms, glb_bytes = gltf.load_scene_glb(scene, tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        source = {"kind": "glb via pt_model_load_gltf (C++ glTF 2.0 loader)", "load_ms": round(load_ms, 1),
+                  "glb_bytes": glb_bytes, "meshes": len(scene.meshes), "textures": len(scene.textures)}
     t0 = time.perf_counter()
     r = setup_renderer(scene, args.width, args.height, args.depth, device=local_rank, kernel=args.kernel)
     r.set_frames_per_launch(args.frames_per_launch)
@@ -530,6 +554,13 @@ def main():
                 "frames_per_launch": args.frames_per_launch,
                 "wavefront_streams": eff_streams,
                 "parallelism": f"spp-shard x{world}",
+                "scene_source": source,
+                # the batches the timed region ran (pt_stats): frames per batch after the queue
+                # budget (pt_set_queue_budget, default a quarter of the device memory) and the
+                # device memory the wavefront queues held
+                "batch_frames": st["last_batch_frames"],
+                "queue_bytes": st["queue_bytes"],
+                "queue_budget_bytes": st["queue_budget"],
                 "bvh_build_ms": round(bvh_ms, 3),  # the first build in the process (code loading included)
                 # pt_options.bvh_builder = PT_BVH_AUTO: the binned-SAH binary tree built on the GPU
                 # (pt_sah_gpu.hip) and collapsed to BVH4 on the GPU; the time above covers both

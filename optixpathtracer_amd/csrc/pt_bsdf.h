@@ -558,7 +558,14 @@ __device__ __forceinline__ f3 bs_weight(const BSample& b) {  // color * |cos| / 
 #else
 #define PT_LAYERED_FN_S __device__ __noinline__
 #endif
-PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+// EXITK = 1: the caller guarantees same_hemisphere(wo, wi) (the light on the viewer's side of the
+// shading plane, nearly every NEE item), so the exit interface is the top one and the walk
+// alternates bottom (even depths) and top (odd depths) at compile time; EXITK = 0 decides at run
+// time.  Both run the same operations on the same values as GlossyDiffuse::f.
+// TOPK = 1 / 2: the caller guarantees a rough / smooth (alpha < 1e-3) top interface for every lane
+// of the wave (the bucketed NEE queue groups them), so the other kind's code is compiled out.
+template <int EXITK, int TOPK = 0>
+PT_LAYERED_FN_F f3 layered_f_t(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
     // GlossyDiffuse.h:141-367 (mediaAlbedo = 0: the medium branch :269-312 is dead code).
     // The top interface is the rough or smooth dielectric, the bottom the Lambertian.  Terms
     // that depend on one direction only are computed once per direction (TRDir): wo and wi
@@ -567,7 +574,10 @@ PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, 
     const int mode = kRadiance;
     const float thickness = 0.01f;
     const float alpha = sqr(roughness);
-    const bool topSpec = alpha < 1e-3f;
+    const bool topSpec = TOPK == 1 ? false : TOPK == 2 ? true : alpha < 1e-3f;
+    // the dielectric helpers test alpha < 1e-3 themselves: the known answer folds their branches
+    if (TOPK == 1) __builtin_assume(!(alpha < 1e-3f));
+    if (TOPK == 2) __builtin_assume(alpha < 1e-3f);
     const bool botSpec = false;
     f3 f = mk(0, 0, 0);
     if (wo.z < 0.0f) {
@@ -575,14 +585,13 @@ PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, 
         wi = -wi;
     }
     const bool enteredTop = true;
-    const bool same = same_hemisphere(wo, wi);
+    const bool same = EXITK == 1 ? true : same_hemisphere(wo, wi);
     bool exitTop, nonExitTop, exitSpec, nonExitSpec;
     if (same ^ enteredTop) {
         exitSpec = botSpec; nonExitSpec = topSpec; exitTop = false; nonExitTop = true;
     } else {
         exitSpec = topSpec; nonExitSpec = botSpec; exitTop = true; nonExitTop = false;
     }
-    const float exitZ = (same ^ enteredTop) ? 0.0f : thickness;
     TRDir pwo{}, pwi{};
     if (!topSpec) {
         tr_dir_frame(pwo, wo, alpha);
@@ -611,7 +620,6 @@ PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, 
                      : lambert_sample(seed, albedo, false, wis);
         if (bs_bad(ok, wis)) continue;
         f3 beta = bs_weight(wos);
-        float z = enteredTop ? thickness : 0.0f;
         f3 w = wos.dir;
         const float tr_wis = transmittance(thickness, wis.dir);
         float tr_w = transmittance(thickness, w);
@@ -619,13 +627,23 @@ PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, 
         const float lam_nwis = (nonExitTop && !topSpec) ? tr_lambda(-wis.dir, alpha) : 0.0f;
         TRDir cw{};  // lam / g1c (and, for a top sample, the frame) of -w
         bool cw_ok = false;
+// PT_LAYERED_UNROLL 2 (round 6): the depth loop unrolled by two, so the compile-time walk of
+// layered_f_split (bottom at even depths, top at odd ones) needs no per-depth interface select.
+// Interleaved A/B against round 5 (profiles/r06e_ab_spec_*.log): config 3 +2.3 %, Layered +2.4 %,
+// Sponza-class +1.3 %; the walk alone unrolled +1.6 / +1.5 %; the top interface's kind
+// specialised as well (PT_LAYERED_SPLIT 2) +2.5 / +3.1 / 0.0 %
+#ifndef PT_LAYERED_UNROLL
+#define PT_LAYERED_UNROLL 2
+#endif
+#if PT_LAYERED_UNROLL > 1
+#pragma unroll PT_LAYERED_UNROLL
+#endif
         for (int depth = 0; depth < 10; ++depth) {
             if (depth > 3 && save_max(beta) < 0.25f) {
                 float q = gmax(0.0f, 1.0f - save_max(beta));
                 if (rnd(ns) < q) break;
                 beta = beta / (1.0f - q);  // f3 / float: fdiv per channel
             }
-            z = (z == thickness) ? 0.0f : thickness;
             beta = beta * tr_w;
             // The reference branches on z == exitZ (GlossyDiffuse.h:315-360); lanes of a wave
             // disagree on exitZ, so both branches would run every depth.  Here the two
@@ -633,7 +651,10 @@ PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, 
             // non-exit branch predicated around it: the same operations and random numbers.
             // (Flattening the sample and depth loops into one loop of steps, so lanes start
             // their next sample early, was 40 % slower: DESIGN.md §5.)
-            const bool atExit = z == exitZ;
+            // z starts at the top (enteredTop) and flips every depth, so it is 0 at even depths
+            // and `thickness` at odd ones; exitZ is `thickness` when wo and wi share a hemisphere
+            // (the top exits) and 0 otherwise: z == exitZ is a parity test.
+            const bool atExit = same ? (depth & 1) != 0 : (depth & 1) == 0;
             const bool itop = atExit ? exitTop : nonExitTop;
             if (itop && !topSpec && !cw_ok) {
                 tr_dir_lam(cw, -w, alpha);
@@ -697,6 +718,26 @@ PT_LAYERED_FN_F f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, 
         }
     }
     return mk(fdiv(f.x, 5.0f), fdiv(f.y, 5.0f), fdiv(f.z, 5.0f));
+}
+__device__ __forceinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+    return layered_f_t<0>(seed, albedo, roughness, wo, wi);
+}
+// The NEE kernel's entry (PT_LAYERED_SPLIT): a wave whose lanes all have the light on the viewer's
+// side takes the compile-time walk, any other wave the run-time one (same_hemisphere is invariant
+// under the walk's flip of both directions).
+#ifndef PT_LAYERED_SPLIT
+#define PT_LAYERED_SPLIT 1
+#endif
+__device__ __forceinline__ f3 layered_f_split(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+    if (PT_LAYERED_SPLIT && __builtin_amdgcn_ballot_w64(!same_hemisphere(wo, wi)) == 0) {
+        if (PT_LAYERED_SPLIT >= 2) {  // the top interface's kind, wave-uniform in all but a bucket's last wave
+            const bool spec = sqr(roughness) < 1e-3f;
+            if (__builtin_amdgcn_ballot_w64(spec) == 0) return layered_f_t<1, 1>(seed, albedo, roughness, wo, wi);
+            if (__builtin_amdgcn_ballot_w64(!spec) == 0) return layered_f_t<1, 2>(seed, albedo, roughness, wo, wi);
+        }
+        return layered_f_t<1>(seed, albedo, roughness, wo, wi);
+    }
+    return layered_f_t<0>(seed, albedo, roughness, wo, wi);
 }
 
 PT_LAYERED_FN_S bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
@@ -768,7 +809,8 @@ __device__ __forceinline__ bool bsdf_sample(uint32_t& seed, f3 albedo, float rou
     if (conductor) return conductor_sample(seed, albedo, roughness, wo, bs);
     return layered_sample(seed, albedo, roughness, wo, bs);
 }
-template <int MODE>
+// SPLIT: the layered eval through layered_f_split (the bucketed NEE kernel)
+template <int MODE, bool SPLIT = false>
 __device__ __forceinline__ f3 bsdf_f(uint32_t& seed, f3 albedo, float roughness, bool conductor, f3 wo, f3 wi) {
     if (MODE == kModeLambert) return lambert_f(albedo, wo, wi);
     if (MODE == kModeConductor) return conductor_f(albedo, roughness, wo, wi);
@@ -776,9 +818,10 @@ __device__ __forceinline__ f3 bsdf_f(uint32_t& seed, f3 albedo, float roughness,
         float v = dielectric_f(roughness, wo, wi, kRadiance);
         return mk(v, v, v);
     }
-    if (MODE == kModeLayered) return layered_f(seed, albedo, roughness, wo, wi);
+    if (MODE == kModeLayered)
+        return SPLIT ? layered_f_split(seed, albedo, roughness, wo, wi) : layered_f(seed, albedo, roughness, wo, wi);
     if (conductor) return conductor_f(albedo, roughness, wo, wi);
-    return layered_f(seed, albedo, roughness, wo, wi);
+    return SPLIT ? layered_f_split(seed, albedo, roughness, wo, wi) : layered_f(seed, albedo, roughness, wo, wi);
 }
 
 }  // namespace pt

@@ -1287,7 +1287,7 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene 
         d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
     }
     const float cosl = abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
-    f3 f = bsdf_f<MODE>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
+    f3 f = bsdf_f<MODE, true>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
     f3 spectrum = f * cosl;
     const float4 bv = W.beta[path];
     const f3 beta = mk(bv.x, bv.y, bv.z);

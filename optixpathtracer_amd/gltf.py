@@ -81,6 +81,108 @@ def load_gltf(path, lights=None, camera_blender_pos=(0.0, 0.0, 0.0), camera_blen
                  name=str(path), textures=textures)
 
 
+def write_glb(scene: Scene, path) -> int:
+    """Write a `scenes.Scene` as one binary glTF 2.0 file (.glb): a JSON chunk and a BIN chunk with
+    float32 POSITION / NORMAL / TEXCOORD_0, uint32 indices, the node matrix (column-major, the
+    model matrix ModelLoader reads back, ModelLoader.cpp:199-245), the metallic-roughness material
+    (baseColorFactor, metallicFactor, roughnessFactor, baseColorTexture, metallicRoughnessTexture,
+    normalTexture; ModelLoader.cpp:171-197) and the RGBA8 textures embedded as PNG buffer views.
+    The reference has no writer; this is the tool that hands the procedural scenes to the
+    loader (pt_model_load_gltf) at full size.  Every value round-trips exactly (float32 in,
+    float32 out).  Returns the file size in bytes."""
+    import json
+    import struct
+    from pathlib import Path
+
+    from PIL import Image
+
+    chunks, views, accessors, meshes, nodes, materials, images = [], [], [], [], [], [], []
+    off = 0
+
+    def view(data: bytes) -> int:
+        nonlocal off
+        pad = (4 - len(data) % 4) % 4
+        views.append({"buffer": 0, "byteOffset": off, "byteLength": len(data)})
+        chunks.append(data + b"\0" * pad)
+        off += len(data) + pad
+        return len(views) - 1
+
+    def accessor(arr, ctype, typ, count, minmax=False) -> int:
+        a = {"bufferView": view(np.ascontiguousarray(arr).tobytes()), "componentType": ctype, "count": count,
+             "type": typ}
+        if minmax:  # POSITION needs its bounds (glTF 2.0 3.6.2.4)
+            a["min"] = [float(x) for x in np.asarray(arr).min(axis=0)]
+            a["max"] = [float(x) for x in np.asarray(arr).max(axis=0)]
+        accessors.append(a)
+        return len(accessors) - 1
+
+    for m in scene.meshes:
+        v = np.asarray(m.vertices, np.float32)
+        attrs = {"POSITION": accessor(v, 5126, "VEC3", len(v), minmax=len(v) > 0)}
+        if m.normals is not None:
+            attrs["NORMAL"] = accessor(np.asarray(m.normals, np.float32), 5126, "VEC3", len(m.normals))
+        if m.texcoords is not None:
+            attrs["TEXCOORD_0"] = accessor(np.asarray(m.texcoords, np.float32), 5126, "VEC2", len(m.texcoords))
+        idx = np.asarray(m.indices, np.uint32).ravel()
+        pbr = {"baseColorFactor": [float(c) for c in m.albedo] + [1.0], "metallicFactor": float(m.metallic),
+               "roughnessFactor": float(m.roughness)}
+        mat = {"pbrMetallicRoughness": pbr}
+        if m.albedo_tex >= 0:
+            pbr["baseColorTexture"] = {"index": int(m.albedo_tex)}
+        if m.metal_rough_tex >= 0:
+            pbr["metallicRoughnessTexture"] = {"index": int(m.metal_rough_tex)}
+        if m.normal_tex >= 0:
+            mat["normalTexture"] = {"index": int(m.normal_tex)}
+        materials.append(mat)
+        prim = {"attributes": attrs, "indices": accessor(idx, 5125, "SCALAR", int(idx.size)),
+                "material": len(materials) - 1}
+        meshes.append({"primitives": [prim]})
+        nodes.append({"name": m.name, "mesh": len(meshes) - 1,
+                      "matrix": [float(x) for x in np.asarray(m.model, np.float32).ravel()]})
+    for t in scene.textures:
+        px = np.ascontiguousarray(t, dtype=np.uint32).view(np.uint8).reshape(t.shape[0], t.shape[1], 4)
+        buf = io.BytesIO()
+        Image.fromarray(px, "RGBA").save(buf, "PNG")
+        images.append({"bufferView": view(buf.getvalue()), "mimeType": "image/png"})
+    binbuf = b"".join(chunks)
+    doc = {"asset": {"version": "2.0", "generator": "optixpathtracer_amd.gltf.write_glb"}, "scene": 0,
+           "scenes": [{"nodes": list(range(len(nodes)))}], "nodes": nodes, "meshes": meshes,
+           "materials": materials, "accessors": accessors, "bufferViews": views,
+           "buffers": [{"byteLength": len(binbuf)}]}
+    if images:
+        doc["images"] = images
+        doc["textures"] = [{"source": k} for k in range(len(images))]
+    js = json.dumps(doc, separators=(",", ":")).encode()
+    js += b" " * ((4 - len(js) % 4) % 4)
+    total = 12 + 8 + len(js) + 8 + len(binbuf)
+    with open(Path(path), "wb") as f:
+        f.write(struct.pack("<4sII", b"glTF", 2, total))
+        f.write(struct.pack("<II", len(js), 0x4E4F534A))
+        f.write(js)
+        f.write(struct.pack("<II", len(binbuf), 0x004E4942))
+        f.write(binbuf)
+    return total
+
+
+def load_scene_glb(scene: Scene, folder) -> tuple:
+    """`scene` written to `folder`/<name>.glb (write_glb) and loaded back through the C++ loader:
+    (loaded scene, pt_model_load_gltf wall ms, file bytes).  The lights, camera and material mode
+    come from `scene`, as the reference's Scene presets set them beside the loaded model
+    (main.cpp:6-78)."""
+    import time
+    from pathlib import Path
+
+    p = Path(folder) / f"{scene.name or 'scene'}.glb"
+    size = write_glb(scene, p)
+    t = time.perf_counter()
+    loaded = load_gltf(p, lights=scene.lights, camera_blender_pos=scene.camera_blender_pos,
+                       camera_blender_rot=scene.camera_blender_rot, fov_deg=scene.fov_deg,
+                       material_mode=scene.material_mode, use_pil=False)
+    ms = (time.perf_counter() - t) * 1e3
+    loaded.name = scene.name
+    return loaded, ms, size
+
+
 def decode_png(data: bytes) -> np.ndarray:
     """The loader's PNG decoder: (H, W, 4) uint8 RGBA, rows as stored."""
     lib = load()

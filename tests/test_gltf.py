@@ -266,3 +266,37 @@ def test_load_gltf_rejects_malformed(tmp_path, name):
 def test_minimal_gltf_loads(tmp_path):
     sc = gltf.load_gltf(_minimal(tmp_path, lambda d: None))
     assert sc.n_triangles == 1
+
+
+def _same_scene(a, b):
+    assert len(a.meshes) == len(b.meshes) and len(a.textures) == len(b.textures)
+    for ma, mb in zip(a.meshes, b.meshes):
+        np.testing.assert_array_equal(np.asarray(ma.vertices, np.float32), mb.vertices)
+        np.testing.assert_array_equal(np.asarray(ma.indices, np.int32), mb.indices)
+        for fa, fb in ((ma.normals, mb.normals), (ma.texcoords, mb.texcoords)):
+            assert (fa is None) == (fb is None)
+            if fa is not None:
+                np.testing.assert_array_equal(np.asarray(fa, np.float32), fb)
+        np.testing.assert_array_equal(np.asarray(ma.model, np.float32), mb.model)
+        assert np.float32(ma.metallic) == np.float32(mb.metallic)
+        assert np.float32(ma.roughness) == np.float32(mb.roughness)
+        np.testing.assert_array_equal(np.float32(ma.albedo), np.float32(mb.albedo))
+        assert (ma.albedo_tex, ma.normal_tex, ma.metal_rough_tex) == (mb.albedo_tex, mb.normal_tex, mb.metal_rough_tex)
+        assert ma.name == mb.name
+    for ta, tb in zip(a.textures, b.textures):
+        np.testing.assert_array_equal(ta, tb)
+
+
+@pytest.mark.parametrize("name", ["textured_conductor", "sponza_class", "sponza_textured"])
+def test_write_glb_round_trip(tmp_path, name):
+    """the procedural scenes written as one .glb (gltf.write_glb, embedded
+    PNG textures) and read back by the C++ loader (pt_model_load_gltf, ModelLoader::LoadModel's
+    counterpart) give the same meshes, materials and textures bit for bit -- at full size for the
+    250k-triangle atria (configs[4]), so bench.py --config 5 / 5t render the loaded scenes."""
+    from optixpathtracer_amd import gltf, scenes
+
+    sc = scenes.make_scene(name)
+    loaded, ms, size = gltf.load_scene_glb(sc, tmp_path)
+    assert size > 0 and ms > 0
+    _same_scene(sc, loaded)
+    assert loaded.n_triangles == sc.n_triangles and loaded.material_mode == sc.material_mode

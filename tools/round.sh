@@ -18,7 +18,7 @@ if [ "$PART" = bench ]; then
   echo "[round] gpu tests"
   timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/gputest.log" 2>&1
   tail -1 "$OUT/gputest.log"
-  for c in 2 3 4l 5 4d; do
+  for c in 2 3 4l 5 5t 4d; do
     echo "[round] bench config $c"
     timeout -k 10 300 python3 bench.py --config $c > "$OUT/bench_config$c.json" 2> "$OUT/bench_config$c.log"
     cat "$OUT/bench_config$c.json"
