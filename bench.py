@@ -135,6 +135,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"),
                     help="PMC traffic per launch measured by tools/profile.sh (optional)")
+    ap.add_argument("--queue-budget", type=int, default=0,
+                    help="pt_set_queue_budget: bytes for all streams' wavefront queues (0 = the library's "
+                         "default, a quarter of the device memory; -1 = none)")
     ap.add_argument("--wavefront-streams", type=int, default=0,
                     help="streams the wavefront batches alternate between (pt_set_wavefront_streams; "
                          "0 = the library's auto: two for Conductor and Dielectric, one otherwise)")
@@ -226,6 +229,7 @@ def main():
     r = setup_renderer(scene, args.width, args.height, args.depth, device=local_rank, kernel=args.kernel)
     r.set_frames_per_launch(args.frames_per_launch)
     r.set_wavefront_streams(args.wavefront_streams)
+    r.set_queue_budget(args.queue_budget)
     # the streams the timed region runs on: 0 is the library's auto (one for Lambert, two otherwise)
     eff_streams = args.wavefront_streams or (2 if scene.material_mode in (2, 3) else 1)
     if args.kernel != 0:  # wavefront (auto resolves to it): time every k_extend launch

@@ -227,6 +227,13 @@ int pt_set_queue_budget(pt_renderer* r, int64_t bytes);
    kernel that waits until the batch is cancelled (a state change), the hold is switched off, or
    10 s pass, so a test can change the state while the batch is provably in flight. */
 int pt_set_debug_hold(pt_renderer* r, int32_t on);
+/* Diagnostics (counted while pt_set_traversal_stats is on, since pt_stats_reset): how coherent the
+   wavefront trace kernels' global BVH node loads are.  For every wave step in which some lanes
+   load a node from global memory (not from the LDS-staged top levels), the number of distinct
+   nodes those lanes load: hist[0..5] = steps with 1, 2, 3-4, 5-8, 9-16, 17-64 distinct nodes,
+   hist[6] = all such steps, hist[7] = the lanes that loaded a global node (VERDICT round 5
+   item 5: a wave-uniform scalar-cache node fetch pays only if few distinct nodes are common). */
+int pt_get_trace_coherence(pt_renderer* r, uint64_t hist[8]);
 /* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */
 int pt_set_traversal_stats(pt_renderer* r, int32_t enable);
 /* Bracket every wavefront trace launch (k_extend, k_trace_pair) with its own HIP event pair

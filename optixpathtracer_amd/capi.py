@@ -183,6 +183,7 @@ SIGNATURES = {
     "pt_set_render_ahead": (C.c_int, [_R, C.c_int32]),
     "pt_set_render_ahead_budget": (C.c_int, [_R, C.c_float]),
     "pt_set_queue_budget": (C.c_int, [_R, C.c_int64]),
+    "pt_get_trace_coherence": (C.c_int, [_R, C.POINTER(C.c_uint64)]),
     "pt_set_debug_hold": (C.c_int, [_R, C.c_int32]),
     "pt_set_traversal_stats": (C.c_int, [_R, C.c_int32]),
     "pt_set_kernel_timing": (C.c_int, [_R, C.c_int32]),

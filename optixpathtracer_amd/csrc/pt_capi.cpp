@@ -90,7 +90,7 @@ struct EventPool {
 // [9..13] wave schedule of the trace kernels (pt_stats wave_*) [14] node visits served from LDS
 // [15] items of the timed shading kernel (pt_stats shade_kernel_items) [16] [17] rays and
 // algorithmic bytes of the k_trace_pair launches alone (pt_stats pair_kernel_*).
-constexpr int kCounters = 20;
+constexpr int kCounters = 28;  // [20..26]: trace coherence histogram (pt_get_trace_coherence)
 // event pairs held by one renderer before launch_frames retires them (EventPool)
 constexpr size_t kMaxPendingEvents = 4096;
 // the smallest traversal stack of any kernel (pt_device.h stack_capacity: 71 entries for the
@@ -1730,6 +1730,22 @@ int pt_set_frames_per_launch(pt_renderer* r, int32_t frames) {
         p->frames_per_launch = frames;
         p->nf_fit = 0;
     }
+    return PT_OK;
+}
+
+int pt_get_trace_coherence(pt_renderer* r, uint64_t hist[8]) {
+    if (!r || !hist) return fail(PT_ERR_INVALID, "pt_get_trace_coherence: NULL");
+    int rc = pt_synchronize(r);
+    if (rc) return rc;
+    unsigned long long c[kCounters];
+    PT_HIP(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost), "download counters");
+    uint64_t steps = 0;
+    for (int k = 0; k < 6; ++k) {
+        hist[k] = c[20 + k];
+        steps += c[20 + k];
+    }
+    hist[6] = steps;
+    hist[7] = c[26];
     return PT_OK;
 }
 

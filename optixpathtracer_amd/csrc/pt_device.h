@@ -130,6 +130,11 @@ struct TravStats {
     // wave schedule (trace_range, lane 0 of each wave): iterations, active lanes summed over
     // them, iterations running the node half / the triangle half, refill blocks
     uint32_t steps = 0, active = 0, node_steps = 0, tri_steps = 0, refills = 0;
+    // coherence of the global (non-LDS) node loads: per wave step with
+    // such loads, the number of distinct nodes its lanes load, in buckets 1, 2, 3-4, 5-8, 9-16,
+    // 17-64 (wave-uniform, counted by every lane alike), and the lanes that loaded one
+    uint32_t coh[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t coh_lanes = 0;
 #if PT_CYCLE_PROBE
     uint64_t probe_t = 0;  // s_memtime when the node half's loads landed
 #endif

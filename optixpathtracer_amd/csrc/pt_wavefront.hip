@@ -157,6 +157,8 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
         atomicAdd(&counters[13], (unsigned long long)ts.refills);
         atomicAdd(&counters[14], l);
         atomicAdd(&counters[18], u);
+        for (int k = 0; k < 6; ++k) atomicAdd(&counters[20 + k], (unsigned long long)ts.coh[k]);
+        atomicAdd(&counters[26], (unsigned long long)ts.coh_lanes);
     }
 }
 
@@ -618,6 +620,20 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
         const uint64_t c2 = probe_clock(st.best);
         if (STATS) ts.tri_steps += (uint32_t)(c2 - c1);
 #endif
+        if (STATS) {  // distinct global nodes among the lanes about to load one (pt_get_trace_coherence)
+            const bool g = active && !done && st.cur >= S.n_lds;
+            unsigned long long rem = __ballot(g);
+            if (rem) {
+                ts.coh_lanes += (uint32_t)__popcll(rem);
+                int distinct = 0;
+                while (rem) {
+                    const int node = __shfl(st.cur, __ffsll((long long)rem) - 1, 64);
+                    rem &= ~__ballot(g && st.cur == node);
+                    ++distinct;
+                }
+                ts.coh[distinct <= 2 ? distinct - 1 : distinct <= 4 ? 2 : distinct <= 8 ? 3 : distinct <= 16 ? 4 : 5]++;
+            }
+        }
         if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockTrace, spill, ts)) done = true;
 #if PT_CYCLE_PROBE
         if (STATS) {  // node half: until its loads landed (active), the rest (node_steps)

@@ -184,6 +184,14 @@ class OptixRenderer:
         device memory; < 0 = none)."""
         check(self.lib.pt_set_queue_budget(self.h, int(nbytes)), "pt_set_queue_budget")
 
+    def trace_coherence(self) -> dict:
+        """pt_get_trace_coherence: wave steps of the trace kernels by the number of distinct global
+        BVH nodes their lanes load (counted while traversal stats are on)."""
+        h = (C.c_uint64 * 8)()
+        check(self.lib.pt_get_trace_coherence(self.h, h), "pt_get_trace_coherence")
+        keys = ["d1", "d2", "d3_4", "d5_8", "d9_16", "d17_64", "steps", "lanes"]
+        return {k: int(v) for k, v in zip(keys, h)}
+
     def set_debug_hold(self, on: bool) -> None:
         """pt_set_debug_hold (tests): speculative look-ahead batches wait until cancelled or released."""
         check(self.lib.pt_set_debug_hold(self.h, 1 if on else 0), "pt_set_debug_hold")
