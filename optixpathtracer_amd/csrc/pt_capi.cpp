@@ -202,6 +202,7 @@ struct pt_renderer {
     bool kernel_timing = false;
     bool primary_dedup = true;  // pt_set_primary_dedup
     bool band_split = true;     // pt_set_band_split: one-frame calls render two row bands on two streams
+    bool wide_trace = true;     // one-stream calls: wide trace workgroups (PT_WIDE_TRACE env 0 turns it off)
     EventPool tev;
     std::vector<hipEvent_t> tev_frame;  // 2 * (max_bounces + 1) events handed to one frame
     double trace_ms = 0.0;
@@ -562,7 +563,8 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
                                           nf, r->primary_dedup, dev_cus, st, tev, &n_timed,
                                           // batches add into the sum in frame order; bands touch disjoint pixels
                                           dual && batch > 0 && nband == 1 ? r->ev_accum[(batch - 1) & 1] : nullptr,
-                                          dual && nband == 1 ? r->ev_accum[batch & 1] : nullptr, sev, &n_stimed),
+                                          dual && nband == 1 ? r->ev_accum[batch & 1] : nullptr, sev, &n_stimed,
+                                          ns == 1 && r->wide_trace),
                    "wavefront launch");
             if (tev) {  // pairs never recorded (the last ones handed out)
                 const int unused = r->max_bounces + 1 - n_timed;
@@ -1059,6 +1061,8 @@ int pt_create(const pt_scene* scene, const pt_options* options, pt_renderer** ou
     }
 
     pt_renderer* r = new pt_renderer();
+    // A/B switch for the wide trace workgroups (tools/ab.sh runs one library with and without)
+    if (const char* e = std::getenv("PTAMD_WIDE_TRACE")) r->wide_trace = std::atoi(e) != 0;
     r->device = opt.device;
     r->material_mode = opt.material_mode;
     r->kernel = opt.kernel;

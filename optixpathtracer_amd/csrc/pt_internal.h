@@ -103,12 +103,14 @@ void wavefront_free(WFState& W);
 // primary_dedup: trace the batch's identical camera rays once per pixel (k_extend `dup`).
 // accum_wait / accum_done (optional): the batch's k_accum waits for accum_wait and records
 // accum_done, so batches on different streams still add into the sum in frame order.
+// wide_trace: the call runs on one stream, so the untextured trace kernels take the wide
+// workgroups (pt_wavefront.hip kBlockTraceWide).
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
                                   const hipEvent_t* trace_events,
                                   int* n_timed = nullptr, hipEvent_t accum_wait = nullptr,
                                   hipEvent_t accum_done = nullptr, const hipEvent_t* shade_events = nullptr,
-                                  int* n_shade_timed = nullptr);
+                                  int* n_shade_timed = nullptr, bool wide_trace = false);
 
 // Render launches.
 hipError_t launch_render(int kernel, int mode, bool stats, const DevScene& S, const DevLaunch& L,

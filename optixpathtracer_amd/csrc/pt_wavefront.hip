@@ -60,8 +60,22 @@ constexpr int kStack = PT_WF_STACK;
 #define PT_LDS_NODES 49
 #endif
 constexpr int kLdsNodes = PT_LDS_NODES;
+// Wide trace workgroups (round 6): on one wavefront stream (Lambert, Default, Layered) the untextured
+// trace kernels run 768-thread workgroups, two per CU, each staging 150 top nodes (levels 0-3 and 65
+// of level 4) in LDS instead of six 256-thread workgroups with 49 each: the same 6 waves per SIMD,
+// three times the staged nodes per workgroup.  Lambert +2.5 %, Default +0.6 %, Sponza-class +1.0 %;
+// beside a second stream's shading kernels (Conductor, Dielectric) the 256-thread workgroups stay
+// (Dielectric 3404 on two streams vs 3362 with wide workgroups on one).
+#ifndef PT_TRACE_BLOCK_WIDE
+#define PT_TRACE_BLOCK_WIDE 768
+#endif
+#ifndef PT_LDS_NODES_WIDE
+#define PT_LDS_NODES_WIDE 150
+#endif
+constexpr int kBlockTraceWide = PT_TRACE_BLOCK_WIDE;
+template <int BLK>
+constexpr int lds_nodes_of() { return BLK == kBlockTrace ? kLdsNodes : PT_LDS_NODES_WIDE; }
 // wave-batched triangle tests (pt_device.h wave_tri_batch): 2.25 KB of LDS per wave
-constexpr int kTriBatchWaves = kBlockTrace / 64;
 // Trace kernels: 6 waves per SIMD (80 VGPRs, 3 spilled in cold paths); the textured variants
 // keep 4.
 #ifndef PT_WF_WAVES
@@ -261,6 +275,58 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     __syncthreads();
     return lds[WAVES] + lds[wave] + prefix;
 }
+
+// Block-wide append with one atomic per block whose slots are ordered by key: the block's range
+// holds its key-0 items first, then key 1, ... (thread order within a key); key < 0 appends
+// nothing.  Consecutive queue entries then share their key (the shadow rays' light, the
+// continuation rays' direction octant), so the trace kernels' waves trace rays that take similar
+// paths through the BVH.  `lds` holds K * WAVES + K + 1 ints.
+template <int WAVES, int K>
+__device__ __forceinline__ int block_append_sorted(int* counter, int key, int* lds) {
+    const int wave = threadIdx.x >> 6;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const unsigned long long m = __ballot(key == k ? 1 : 0);
+        if (key == k) mine = m;
+        if (lane_id() == 0) lds[k * WAVES + wave] = __popcll(m);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < K) {  // per key: the waves' exclusive prefix and the key's total
+        const int k = threadIdx.x;
+        int tot = 0;
+        for (int w = 0; w < WAVES; ++w) {
+            const int c = lds[k * WAVES + w];
+            lds[k * WAVES + w] = tot;
+            tot += c;
+        }
+        lds[K * WAVES + 1 + k] = tot;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the keys' exclusive prefix, one atomic for the block
+        int tot = 0;
+        for (int k = 0; k < K; ++k) {
+            const int c = lds[K * WAVES + 1 + k];
+            lds[K * WAVES + 1 + k] = tot;
+            tot += c;
+        }
+        lds[K * WAVES] = tot > 0 ? atomicAdd(counter, tot) : 0;
+    }
+    __syncthreads();
+    if (key < 0) return 0;
+    const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    return lds[K * WAVES] + lds[K * WAVES + 1 + key] + lds[key * WAVES + wave] + pre;
+}
+// PT_SORT_SHADOW / PT_SORT_EXT: the fused shading kernels append their shadow rays ordered by light
+// and their continuation rays ordered by direction octant within each block (block_append_sorted)
+#ifndef PT_SORT_SHADOW
+#define PT_SORT_SHADOW 0
+#endif
+#ifndef PT_SORT_EXT
+#define PT_SORT_EXT 0
+#endif
+constexpr int kSortKeys = 8;
+__device__ __forceinline__ int octant(f3 d) { return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0); }
 
 // Block-wide append into K bucket regions (counter of bucket k at counter0 + k * kCntStride):
 // threads with bucket k in [0, K) get consecutive slots of region k in thread order, bucket < 0
@@ -512,7 +578,7 @@ struct NoCommit {
     template <class T>
     __device__ void operator()(const T&) const {}
 };
-template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
+template <int ANY, bool STATS, bool TEX, int BLK, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end, int* stk, TriBatchLds* tri_lds,
                                             TravStats& ts, const WFState& W, Fetch fetch, Finish finish,
                                             Commit commit = Commit{}, RayPool pool = RayPool{}) {
@@ -634,7 +700,7 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
                 ts.coh[distinct <= 2 ? distinct - 1 : distinct <= 4 ? 2 : distinct <= 8 ? 3 : distinct <= 16 ? 4 : 5]++;
             }
         }
-        if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, kBlockTrace, spill, ts)) done = true;
+        if (active && !done && trav_node_step<ANY, STATS, kStack>(S, st, stk, BLK, spill, ts)) done = true;
 #if PT_CYCLE_PROBE
         if (STATS) {  // node half: until its loads landed (active), the rest (node_steps)
             const uint64_t c4 = probe_clock(st.cur);
@@ -649,18 +715,19 @@ __device__ __forceinline__ void trace_range(const DevScene& S, int next, int end
 
 // A trace kernel's queue range [first, end): the workgroup's LDS (per-lane stacks, the staged top
 // BVH levels, the triangle batches), then the lane-refilling loop.
-template <int ANY, bool STATS, bool TEX, class Fetch, class Finish, class Commit = NoCommit>
+template <int ANY, bool STATS, bool TEX, int BLK, class Fetch, class Finish, class Commit = NoCommit>
 __device__ __forceinline__ void trace_queue(DevScene S, int first, int end, TravStats& ts, const WFState& W, Fetch fetch,
                                             Finish finish, Commit commit = Commit{}, RayPool pool = RayPool{}) {
-    __shared__ int stack[kStack * kBlockTrace];
-    __shared__ BNode4 top[kLdsNodes > 0 ? kLdsNodes : 1];
-    __shared__ TriBatchLds tri_batch[kTriBatchWaves];
-    stage_top_nodes<kLdsNodes>(S, top);
-    trace_range<ANY, STATS, TEX>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, W, fetch,
-                                 finish, commit, pool);
+    constexpr int kNodes = lds_nodes_of<BLK>();
+    __shared__ int stack[kStack * BLK];
+    __shared__ BNode4 top[kNodes > 0 ? kNodes : 1];
+    __shared__ TriBatchLds tri_batch[BLK / 64];
+    stage_top_nodes<kNodes>(S, top);
+    trace_range<ANY, STATS, TEX, BLK>(S, first, end, stack + threadIdx.x, tri_batch + (threadIdx.x >> 6), ts, W, fetch,
+                                      finish, commit, pool);
 }
 
-template <int ANY, bool STATS, bool TEX, class Fetch, class Finish>
+template <int ANY, bool STATS, bool TEX, int BLK, class Fetch, class Finish>
 __device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats& ts, const WFState& W, Fetch fetch,
                                             Finish finish, int* pool_ctr) {
     int next, end;
@@ -674,7 +741,7 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats&
         pool.begin = n;
     }
     wave_slice(pool.begin, next, end, pool.chunk_log);
-    trace_queue<ANY, STATS, TEX>(S, next, end, ts, W, fetch, finish, NoCommit{}, pool);
+    trace_queue<ANY, STATS, TEX, BLK>(S, next, end, ts, W, fetch, finish, NoCommit{}, pool);
 }
 
 // Closest hit of queue b.  `dup` > 1 (bounce 0 only): the queue holds `dup` copies of the same
@@ -682,15 +749,15 @@ __device__ __forceinline__ void trace_slice(const DevScene& S, int n, TravStats&
 // is identical in every frame, devicePrograms.cu:601-623), so only the first n / dup are traced
 // and each hit record is written to all copies.  The records are bit-identical to tracing every
 // copy; DESIGN.md §5 gives the A/B.
-template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_extend(DevScene S, WFState W, int b, int dup,
+template <bool STATS, bool TEX, int BLK = kBlockTrace>
+__global__ __launch_bounds__(BLK, wf_waves(TEX)) void k_extend(DevScene S, WFState W, int b, int dup,
                                                                   int copies, unsigned long long* counters) {
     const int n = *cnt(W, b, kQueue);
     const int n_trace = n / dup;
     const float4* ro = W.ray_o[b & 1];
     const float4* rd = W.ray_d[b & 1];
     TravStats ts;
-    trace_slice<kRayClosest, STATS, TEX>(
+    trace_slice<kRayClosest, STATS, TEX, BLK>(
         S, n_trace, ts, W,
         [&](int ri, TravState& st) {
             const float4 a = ldq_x(ro + ri), c = ldq_x(rd + ri);
@@ -799,7 +866,7 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
     const float4* rd = W.ray_d[b & 1];
     float4* no = W.ray_o[(b + 1) & 1];
     float4* nd = W.ray_d[(b + 1) & 1];
-    __shared__ int lds_sh[kWaves + 1], lds_q[kWaves + 1];
+    __shared__ int lds_sh[kSortKeys * kWaves + kSortKeys + 1], lds_q[kSortKeys * kWaves + kSortKeys + 1];
     if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters) atomicAdd(&L.counters[15], (unsigned long long)n);
     if ((int)(blockIdx.x * kBlock) >= n) return;  // block-uniform
     {
@@ -811,6 +878,7 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
         uint32_t seed = 0;
         float stmax = 0.0f;
         int path = 0;
+        int shadow_light = 0;
         const int P1 = L.width * L.height;
         float4 l0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // shade0: the path's radiance after bounce 0
         if (valid) {
@@ -867,6 +935,7 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
                             sdir = normalize(ldir);
                             stmax = length(ldir);
                             emit_shadow = true;
+                            shadow_light = li;
                         }
                     }
                 }
@@ -880,13 +949,16 @@ __global__ __launch_bounds__(shf_block(MODE), shf_waves(MODE)) void k_shade_fuse
             }
         }
         if (shade0 && valid) W.L[path] = l0;  // every path of the batch, hit or miss
-        const int qi = block_append<kWaves>(cnt(W, b + 1, kQueue), emit_next, lds_q);
+        const int qi = PT_SORT_EXT ? block_append_sorted<kWaves, kSortKeys>(cnt(W, b + 1, kQueue), emit_next ? octant(d) : -1, lds_q)
+                                   : block_append<kWaves>(cnt(W, b + 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
             if (kBetaQ) stqs(queue_beta(W, b + 1) + qi, make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed)));
         }
-        const int si = block_append<kWaves>(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
+        const int si = PT_SORT_SHADOW ? block_append_sorted<kWaves, kSortKeys>(cnt(W, b, kShadowQ),
+                                                                              emit_shadow ? (shadow_light & (kSortKeys - 1)) : -1, lds_sh)
+                                      : block_append<kWaves>(cnt(W, b, kShadowQ), emit_shadow, lds_sh);
         if (emit_shadow) {
             // Lambert: a sampled direction is never below the surface (lambert_sample forces z >= 0),
             // so the continuation ray starts at the shadow ray's origin (sf.pos + 1e-3 * Ng, the
@@ -910,7 +982,7 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
     constexpr bool kBetaQ = MODE == kModeLambert;  // as k_shade_fused
     constexpr int kBlock = shf_block(MODE), kWaves = kBlock / 64;
     const int P1 = L.width * L.height;
-    __shared__ int lds_q[kWaves + 1];
+    __shared__ int lds_q[kSortKeys * kWaves + kSortKeys + 1];
     if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters)
         atomicAdd(&L.counters[15], (unsigned long long)P1 * (unsigned long long)nf);
     if ((int)(blockIdx.x * kBlock) >= P1) return;  // block-uniform
@@ -963,7 +1035,8 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
             }
         }
         if (valid) stqs(W.L + path, l0);  // every path of the batch, hit or miss
-        const int qi = block_append<kWaves>(cnt(W, 1, kQueue), emit_next, lds_q);
+        const int qi = PT_SORT_EXT ? block_append_sorted<kWaves, kSortKeys>(cnt(W, 1, kQueue), emit_next ? octant(d) : -1, lds_q)
+                                   : block_append<kWaves>(cnt(W, 1, kQueue), emit_next, lds_q);
         if (emit_next) {
             stqs(no + qi, make_float4(o.x, o.y, o.z, __int_as_float(path)));
             stqs(nd + qi, make_float4(d.x, d.y, d.z, 0.0f));
@@ -976,8 +1049,8 @@ __global__ __launch_bounds__(shf_block(MODE), 1) void k_shade0_pixel(DevScene S,
 // the same hit points and are independent, so one launch traces both queues (one SIMT tail
 // and one launch instead of two).  Items [0, n_ext) are extension rays (closest hit ->
 // hit records), items [n_ext, n_ext + n_sh) shadow rays (any hit -> deferred NEE add).
-template <bool STATS, bool TEX>
-__global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevScene S, WFState W, int b,
+template <bool STATS, bool TEX, int BLK = kBlockTrace>
+__global__ __launch_bounds__(BLK, wf_waves(TEX)) void k_trace_pair(DevScene S, WFState W, int b,
                                                                       unsigned long long* counters) {
 #if PT_TAIL_PROBE
     unsigned long long tp0;
@@ -1072,7 +1145,7 @@ __global__ __launch_bounds__(kBlockTrace, wf_waves(TEX)) void k_trace_pair(DevSc
         pool.begin = pool.end = n_all;
     }
     wave_slice(pool.begin, first, end);
-    trace_queue<kRayMixed, STATS, TEX>(S, first, end, ts, W, fetch, finish, commit, pool);
+    trace_queue<kRayMixed, STATS, TEX, BLK>(S, first, end, ts, W, fetch, finish, commit, pool);
 #if PT_TAIL_PROBE
     tail_probe_end(b);
 #endif
@@ -1157,13 +1230,13 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
 // Any-hit visibility of the shadow queue of bounce b.  table = 1: the bounce-0 (pixel, light)
 // table (k_shadow0_setup), vis[j] = 1 if unoccluded; table = 0: vis[j] = the ray's item code
 // if unoccluded, else -1 (k_nee_compact reads it).
-template <bool TEX>
-__global__ __launch_bounds__(kBlockTrace, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b, int table,
+template <bool TEX, int BLK = kBlockTrace>
+__global__ __launch_bounds__(BLK, wf_waves(false)) void k_shadow_vis(DevScene S, WFState W, int b, int table,
                                                                       unsigned long long* counters) {
     const int n = *cnt(W, b, kShadowQ);
     if (blockIdx.x == 0 && threadIdx.x == 0 && counters) atomicAdd(&counters[5], (unsigned long long)n);
     TravStats ts;
-    trace_slice<kRayAny, false, TEX>(
+    trace_slice<kRayAny, false, TEX, BLK>(
         S, n, ts, W,
         [&](int j, TravState& st) {
             const float4 a = ldq_x(W.sh_o + j), c = ldq_x(W.sh_d + j);
@@ -1431,13 +1504,13 @@ inline dim3 item_grid(int items, int block) { return dim3((unsigned)std::max(1, 
 // Exactly the blocks that are resident at once (occupancy query, cached) — the lane-
 // refilling trace kernels, whose waves each own a static queue slice.
 template <typename K>
-dim3 occupancy_grid(K kernel, int cus) {
+dim3 occupancy_grid(K kernel, int cus, int block = kBlockTrace) {
     static std::unordered_map<const void*, int> cache;
     const void* key = reinterpret_cast<const void*>(kernel);
     auto it = cache.find(key);
     int per_cu = 0;
     if (it == cache.end()) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockTrace, 0) != hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         cache[key] = per_cu;
     } else {
@@ -1576,7 +1649,8 @@ void wavefront_free(WFState& W) {
 hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const DevLaunch& L, const WFState& W,
                                   uint32_t frame, int nf, bool primary_dedup, int cus, hipStream_t stream,
                                   const hipEvent_t* trace_events, int* n_timed, hipEvent_t accum_wait,
-                                  hipEvent_t accum_done, const hipEvent_t* shade_events, int* n_shade_timed) {
+                                  hipEvent_t accum_done, const hipEvent_t* shade_events, int* n_shade_timed,
+                                  bool wide_trace) {
     const int P = L.width * L.height * nf;  // paths in flight
     const int maxb = L.max_bounces;
     hipError_t e = hipSuccess;
@@ -1605,22 +1679,27 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         ++stimed;
         return hipSuccess;
     };
+    // the untextured trace kernels of a one-stream call take the wide workgroups (kBlockTraceWide)
+    const bool wide = wide_trace && !tex;
+#define PT_TRACE_LAUNCH(KERN, BLK, ...) \
+    hipLaunchKernelGGL((KERN), occupancy_grid(KERN, cus, BLK), dim3(BLK), 0, stream, __VA_ARGS__)
     auto extend = [&](int b, int dup, int copies) -> hipError_t {
         hipError_t r;
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
         if (tex) {
             if (stats)
-                hipLaunchKernelGGL((k_extend<true, true>), occupancy_grid(k_extend<true, true>, cus), dim3(kBlockTrace),
-                                   0, stream, S, W, b, dup, copies, L.counters);
+                PT_TRACE_LAUNCH((k_extend<true, true>), kBlockTrace, S, W, b, dup, copies, L.counters);
             else
-                hipLaunchKernelGGL((k_extend<false, true>), occupancy_grid(k_extend<false, true>, cus),
-                                   dim3(kBlockTrace), 0, stream, S, W, b, dup, copies, L.counters);
+                PT_TRACE_LAUNCH((k_extend<false, true>), kBlockTrace, S, W, b, dup, copies, L.counters);
+        } else if (wide) {
+            if (stats)
+                PT_TRACE_LAUNCH((k_extend<true, false, kBlockTraceWide>), kBlockTraceWide, S, W, b, dup, copies, L.counters);
+            else
+                PT_TRACE_LAUNCH((k_extend<false, false, kBlockTraceWide>), kBlockTraceWide, S, W, b, dup, copies, L.counters);
         } else if (stats) {
-            hipLaunchKernelGGL((k_extend<true, false>), occupancy_grid(k_extend<true, false>, cus), dim3(kBlockTrace), 0,
-                               stream, S, W, b, dup, copies, L.counters);
+            PT_TRACE_LAUNCH((k_extend<true, false>), kBlockTrace, S, W, b, dup, copies, L.counters);
         } else {
-            hipLaunchKernelGGL((k_extend<false, false>), occupancy_grid(k_extend<false, false>, cus), dim3(kBlockTrace),
-                               0, stream, S, W, b, dup, copies, L.counters);
+            PT_TRACE_LAUNCH((k_extend<false, false>), kBlockTrace, S, W, b, dup, copies, L.counters);
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
         ++timed;
@@ -1631,17 +1710,18 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
         if (tex) {
             if (stats)
-                hipLaunchKernelGGL((k_trace_pair<true, true>), occupancy_grid(k_trace_pair<true, true>, cus),
-                                   dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
+                PT_TRACE_LAUNCH((k_trace_pair<true, true>), kBlockTrace, S, W, b, L.counters);
             else
-                hipLaunchKernelGGL((k_trace_pair<false, true>), occupancy_grid(k_trace_pair<false, true>, cus),
-                                   dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
+                PT_TRACE_LAUNCH((k_trace_pair<false, true>), kBlockTrace, S, W, b, L.counters);
+        } else if (wide) {
+            if (stats)
+                PT_TRACE_LAUNCH((k_trace_pair<true, false, kBlockTraceWide>), kBlockTraceWide, S, W, b, L.counters);
+            else
+                PT_TRACE_LAUNCH((k_trace_pair<false, false, kBlockTraceWide>), kBlockTraceWide, S, W, b, L.counters);
         } else if (stats) {
-            hipLaunchKernelGGL((k_trace_pair<true, false>), occupancy_grid(k_trace_pair<true, false>, cus),
-                               dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
+            PT_TRACE_LAUNCH((k_trace_pair<true, false>), kBlockTrace, S, W, b, L.counters);
         } else {
-            hipLaunchKernelGGL((k_trace_pair<false, false>), occupancy_grid(k_trace_pair<false, false>, cus),
-                               dim3(kBlockTrace), 0, stream, S, W, b, L.counters);
+            PT_TRACE_LAUNCH((k_trace_pair<false, false>), kBlockTrace, S, W, b, L.counters);
         }
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed + 1], stream)) != hipSuccess) return r;
         ++timed;
@@ -1651,11 +1731,11 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     };
     auto shadow_vis = [&](int b, int table) -> hipError_t {
         if (tex)
-            hipLaunchKernelGGL(k_shadow_vis<true>, occupancy_grid(k_shadow_vis<true>, cus), dim3(kBlockTrace), 0, stream,
-                               S, W, b, table, L.counters);
+            PT_TRACE_LAUNCH((k_shadow_vis<true>), kBlockTrace, S, W, b, table, L.counters);
+        else if (wide)
+            PT_TRACE_LAUNCH((k_shadow_vis<false, kBlockTraceWide>), kBlockTraceWide, S, W, b, table, L.counters);
         else
-            hipLaunchKernelGGL(k_shadow_vis<false>, occupancy_grid(k_shadow_vis<false>, cus), dim3(kBlockTrace), 0,
-                               stream, S, W, b, table, L.counters);
+            PT_TRACE_LAUNCH((k_shadow_vis<false>), kBlockTrace, S, W, b, table, L.counters);
         if (!table) hipLaunchKernelGGL(k_nee_compact, item_grid(P, kBlockSh * kCompactPer), dim3(kBlockSh), 0, stream, W, b);
         return hipGetLastError();
     };
@@ -1715,6 +1795,7 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
                 return e;
         }
     }
+#undef PT_TRACE_LAUNCH
     if (accum_wait && (e = hipStreamWaitEvent(stream, accum_wait, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_accum, item_grid(L.width * L.height, kBlockWF), dim3(kBlockWF), 0, stream, W, L, nf);
     if (accum_done && (e = hipEventRecord(accum_done, stream)) != hipSuccess) return e;

@@ -14,7 +14,8 @@ for f in sys.argv[1:]:
             v = m.group(1)
         elif line.startswith("{") and "msamples_s" in line:
             j = json.loads(line)
-            d[(j.get("scene", ""), j["mode"], v)].append(j["msamples_s"])
+            vv = v + (f"/s{j['streams']}" if j.get("streams") else "")
+            d[(j.get("scene", ""), j["mode"], vv)].append(j["msamples_s"])
     print(f)
     for k in sorted(d, key=lambda k: (k[1], k[2])):
         print(f"  mode {k[1]} {k[2]:10s} {sum(d[k]) / len(d[k]):9.1f}   {[round(x, 1) for x in d[k]]}")
