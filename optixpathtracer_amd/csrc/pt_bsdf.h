@@ -763,7 +763,15 @@ PT_LAYERED_FN_S bool layered_sample(uint32_t& seed, f3 albedo, float roughness, 
     ns = tea16(ns, seed);
     f3 f = bs.color * abs_cos_theta(bs.dir);
     float pdf = bs.pdf;
-    float z = thickness;
+    // z starts at the top and flips every depth (GlossyDiffuse.h:441-447): the bottom at even
+    // depths, the top at odd ones, so the interface is a parity test and, with the loop unrolled
+    // by two (PT_LAYERED_SAMPLE_UNROLL), known at compile time in each copy
+#ifndef PT_LAYERED_SAMPLE_UNROLL
+#define PT_LAYERED_SAMPLE_UNROLL 1
+#endif
+#if PT_LAYERED_SAMPLE_UNROLL > 1
+#pragma unroll PT_LAYERED_SAMPLE_UNROLL
+#endif
     for (int depth = 0; depth < 10; ++depth) {
         float rrBeta = fdiv(save_max(f), pdf);
         if (depth > 3 && rrBeta < 0.25f) {
@@ -772,9 +780,8 @@ PT_LAYERED_FN_S bool layered_sample(uint32_t& seed, f3 albedo, float roughness, 
             pdf *= 1.0f - q;
         }
         if (w.z == 0.0f) return false;
-        z = (z == thickness) ? 0.0f : thickness;
         f = f * transmittance(thickness, w);
-        bool itop = (z == 0.0f) ? false : true;
+        const bool itop = (depth & 1) != 0;
         ok = layer_sample(itop, seed, albedo, roughness, -w, bs, mode, true, true);
         if (bs_bad(ok, bs)) return false;
         f = f * bs.color;
