@@ -81,7 +81,16 @@ constexpr int lds_nodes_of() { return BLK == kBlockTrace ? kLdsNodes : PT_LDS_NO
 #ifndef PT_WF_WAVES
 #define PT_WF_WAVES 6
 #endif
-constexpr int wf_waves(bool tex) { return tex ? 4 : PT_WF_WAVES; }
+// the textured variants: 6 waves as well since round 6 (4 before; the textured atrium, config 5t,
+// +1.6 % at 6, ±0 at 5, profiles/r06_ab/r06m_ab_tex_c5t.log)
+#ifndef PT_WF_WAVES_TEX
+#define PT_WF_WAVES_TEX 6
+#endif
+// PT_WIDE_TEX 1: the textured trace kernels take the wide workgroups as well on one-stream calls
+#ifndef PT_WIDE_TEX
+#define PT_WIDE_TEX 1  // +0.7 % config 5t, +1.0 % on the small textured scene (profiles/r06_ab/r06n_ab_widetex_*.log)
+#endif
+constexpr int wf_waves(bool tex) { return tex ? PT_WF_WAVES_TEX : PT_WF_WAVES; }
 constexpr int kMissTri = -1;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -1680,13 +1689,18 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         return hipSuccess;
     };
     // the untextured trace kernels of a one-stream call take the wide workgroups (kBlockTraceWide)
-    const bool wide = wide_trace && !tex;
+    const bool wide = wide_trace && (!tex || PT_WIDE_TEX);
 #define PT_TRACE_LAUNCH(KERN, BLK, ...) \
     hipLaunchKernelGGL((KERN), occupancy_grid(KERN, cus, BLK), dim3(BLK), 0, stream, __VA_ARGS__)
     auto extend = [&](int b, int dup, int copies) -> hipError_t {
         hipError_t r;
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
-        if (tex) {
+        if (tex && wide && PT_WIDE_TEX) {
+            if (stats)
+                PT_TRACE_LAUNCH((k_extend<true, true, kBlockTraceWide>), kBlockTraceWide, S, W, b, dup, copies, L.counters);
+            else
+                PT_TRACE_LAUNCH((k_extend<false, true, kBlockTraceWide>), kBlockTraceWide, S, W, b, dup, copies, L.counters);
+        } else if (tex) {
             if (stats)
                 PT_TRACE_LAUNCH((k_extend<true, true>), kBlockTrace, S, W, b, dup, copies, L.counters);
             else
@@ -1708,7 +1722,12 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
     auto pair = [&](int b) -> hipError_t {
         hipError_t r;
         if (trace_events && (r = hipEventRecord(trace_events[2 * timed], stream)) != hipSuccess) return r;
-        if (tex) {
+        if (tex && wide && PT_WIDE_TEX) {
+            if (stats)
+                PT_TRACE_LAUNCH((k_trace_pair<true, true, kBlockTraceWide>), kBlockTraceWide, S, W, b, L.counters);
+            else
+                PT_TRACE_LAUNCH((k_trace_pair<false, true, kBlockTraceWide>), kBlockTraceWide, S, W, b, L.counters);
+        } else if (tex) {
             if (stats)
                 PT_TRACE_LAUNCH((k_trace_pair<true, true>), kBlockTrace, S, W, b, L.counters);
             else
@@ -1730,7 +1749,9 @@ hipError_t launch_wavefront_frame(int mode, bool stats, const DevScene& S, const
         return hipGetLastError();
     };
     auto shadow_vis = [&](int b, int table) -> hipError_t {
-        if (tex)
+        if (tex && wide && PT_WIDE_TEX)
+            PT_TRACE_LAUNCH((k_shadow_vis<true, kBlockTraceWide>), kBlockTraceWide, S, W, b, table, L.counters);
+        else if (tex)
             PT_TRACE_LAUNCH((k_shadow_vis<true>), kBlockTrace, S, W, b, table, L.counters);
         else if (wide)
             PT_TRACE_LAUNCH((k_shadow_vis<false, kBlockTraceWide>), kBlockTraceWide, S, W, b, table, L.counters);
