@@ -23,7 +23,7 @@ def main():
     prof, rnd, out = ROOT / "gpurun_out" / f"prof_{tag}", ROOT / "gpurun_out" / f"round_{tag}", ROOT / "profiles"
     if part == "bench":
         cp = [(rnd / "gputest.log", f"{tag}_gputest.log")]
-        cp += [(rnd / f"bench_config{c}.json", f"{tag}_bench_config{c}.json") for c in ("2", "3", "4l", "5", "4d")]
+        cp += [(rnd / f"bench_config{c}.json", f"{tag}_bench_config{c}.json") for c in ("2", "3", "4l", "5", "5t", "4d")]
         for src, dst in cp:
             shutil.copyfile(src, out / dst)
         return
