@@ -451,7 +451,9 @@ int launch_frames(pt_renderer* r, float* accum, uint32_t first, uint32_t n, doub
         for (int k = 0; k < ns; ++k) {
             WFState& w = k ? r->xwf[k] : r->wf;
             // queues larger than the budget's share (a lowered budget) are allocated again, smaller
-            const bool over = budget != SIZE_MAX && w.paths > 0 && (size_t)ns * wavefront_bytes(w.paths, w.max_bounces) > budget;
+            // (a budget below one frame's queues still allows one frame: no reallocation per call)
+            const bool over = budget != SIZE_MAX && w.paths > P &&
+                              (size_t)ns * wavefront_bytes(w.paths, w.max_bounces) > budget;
             if (w.paths < P * nf_cap || w.max_bounces < r->max_bounces || over) {
                 for (int j = 0; j < pt_renderer::kMaxWFStreams; ++j)
                     if (r->wf_stream(j)) PT_HIP(hipStreamSynchronize(r->wf_stream(j)), "hipStreamSynchronize");
