@@ -232,7 +232,8 @@ int pt_set_debug_hold(pt_renderer* r, int32_t on);
    load a node from global memory (not from the LDS-staged top levels), the number of distinct
    nodes those lanes load: hist[0..5] = steps with 1, 2, 3-4, 5-8, 9-16, 17-64 distinct nodes,
    hist[6] = all such steps, hist[7] = the lanes that loaded a global node (VERDICT round 5
-   item 5: a wave-uniform scalar-cache node fetch pays only if few distinct nodes are common). */
+   item 5: a wave-uniform scalar-cache node fetch pays only if few distinct nodes are common).
+   A multi-device renderer sums every device's counts. */
 int pt_get_trace_coherence(pt_renderer* r, uint64_t hist[8]);
 /* Diagnostics: count BVH nodes visited / triangle tests / rays (slower instrumented kernels). */
 int pt_set_traversal_stats(pt_renderer* r, int32_t enable);

@@ -1752,6 +1752,12 @@ int pt_get_trace_coherence(pt_renderer* r, uint64_t hist[8]) {
     }
     hist[6] = steps;
     hist[7] = c[26];
+    for (pt_renderer* p : r->peers) {  // a multi-device renderer: every device's steps
+        uint64_t ph[8];
+        if ((rc = pt_get_trace_coherence(p, ph)) != PT_OK) return rc;
+        for (int k = 0; k < 8; ++k) hist[k] += ph[k];
+    }
+    PT_HIP(hipSetDevice(r->device), "hipSetDevice");
     return PT_OK;
 }
 
