@@ -187,14 +187,29 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
 
 // Per-bounce counters: queue length and shadow-queue length, each on its own 128-B line
 // (appends from different queues never contend for one L2 line).  Zeroed per frame.
-// Default / Layered shading items are queued per bucket (shade_bucket): kShadeBuckets NEE and
+// Default / Layered shading items are queued per bucket (shade_bucket): kNeeBuckets NEE and
 // kShadeBuckets BSDF-sample counters follow the two queue counters.
 constexpr int kShadeBuckets = 3;
-constexpr int kCnt = 5 + 2 * kShadeBuckets;
+// PT_NEE_CROSS (round 6): the NEE items have one more bucket, kNeeCross: layered items whose light
+// lies across the shading plane from the viewer, so that every other layered NEE wave runs the
+// walk's compile-time path (layered_f_split).  Its queue region is bucket 2's, filled from the back
+// (nee_index).  Without it 70 % of Sponza-class's and 45 % of Layered's walk waves held such a
+// lane (4.2 / 1.6 % of the lanes, tools/nee_probe.py) and ran the run-time walk.
+#ifndef PT_NEE_CROSS
+#define PT_NEE_CROSS 1
+#endif
+constexpr int kNeeBuckets = kShadeBuckets + (PT_NEE_CROSS ? 1 : 0);
+constexpr int kNeeCross = kShadeBuckets;
+constexpr int kCnt = 5 + kNeeBuckets + kShadeBuckets;
 constexpr int kCntStride = 32;  // ints per counter = 128 B
 // kPool*: the run-time ray pools of k_trace_pair, k_extend and k_shadow_vis (RayPool)
-enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kShadeBuckets, kPool = 2 + 2 * kShadeBuckets, kPoolExt, kPoolSh };
+enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kNeeBuckets, kPool = 2 + kNeeBuckets + kShadeBuckets, kPoolExt, kPoolSh };
 __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
+// Slot `slot` of NEE bucket q in W.nq: region q, or for kNeeCross the back of region 2 (a bounce
+// queues at most W.paths NEE items in all, so the two ends never meet)
+__device__ __forceinline__ size_t nee_index(const WFState& W, int q, int slot) {
+    return q < kShadeBuckets ? (size_t)q * W.paths + slot : (size_t)kShadeBuckets * W.paths - 1 - slot;
+}
 // Path throughput | seed.  W.beta in path order (the phases of a bounce read it by path), except
 // in the Lambert mode: in queue order next to the ray, ping-pong like ray_o / ray_d (queue b
 // in W.beta for even b, W.beta_q for odd b), so k_shade_fused streams it instead of gathering it
@@ -1180,7 +1195,7 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
     __shared__ int lds_sh[kWavesShA + 1];
-    __shared__ int lds_nee[kShadeBuckets * (kWavesShA + 1)], lds_smp[kShadeBuckets * (kWavesShA + 1)];
+    __shared__ int lds_nee[kNeeBuckets * (kWavesShA + 1)], lds_smp[kShadeBuckets * (kWavesShA + 1)];
     if ((int)(blockIdx.x * kBlockShA) >= n) return;  // block-uniform
     const int i = (int)(blockIdx.x * kBlockShA + threadIdx.x);
     bool emit = false;
@@ -1211,15 +1226,19 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
             // the last bounce's sampled direction is never traced (SamplePath :646): no sample item
             if (b + 1 < L.max_bounces) smp_bucket = bk;
             if (P > 0.0f) {
+                const DevLight lt = L.lights[li];
+                f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
+                const f3 ln = normalize(ldir);  // k_shade_nee's light direction, the same bits
+                int nb = bk;
+                if (PT_NEE_CROSS && (MODE == kModeLayered || !conductor) && !same_hemisphere(sf.wo, to_local(sf.fr, ln)))
+                    nb = kNeeCross;
                 if (vis0) {
-                    if (W.vis[vis0_index(L, path, li)]) nee_bucket = bk;
+                    if (W.vis[vis0_index(L, path, li)]) nee_bucket = nb;
                 } else {
-                    const DevLight lt = L.lights[li];
-                    f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
                     so = sf.pos + 1e-3f * sf.ng;
-                    sdir = normalize(ldir);
+                    sdir = ln;
                     stmax = length(ldir);
-                    code = i | (bk << kItemBits);
+                    code = i | (nb << kItemBits);
                     emit = true;
                 }
             }
@@ -1230,8 +1249,8 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
         W.sh_o[si] = make_float4(so.x, so.y, so.z, __int_as_float(code));
         W.sh_d[si] = make_float4(sdir.x, sdir.y, sdir.z, stmax);
     }
-    const int ni = block_append_k<kWavesShA, kShadeBuckets>(cnt(W, b, kNee0), nee_bucket, lds_nee);
-    if (nee_bucket >= 0) W.nq[(size_t)nee_bucket * W.paths + ni] = i;
+    const int ni = block_append_k<kWavesShA, kNeeBuckets>(cnt(W, b, kNee0), nee_bucket, lds_nee);
+    if (nee_bucket >= 0) W.nq[nee_index(W, nee_bucket, ni)] = i;
     const int mi = block_append_k<kWavesShA, kShadeBuckets>(cnt(W, b, kSmp0), smp_bucket, lds_smp);
     if (smp_bucket >= 0) W.sq[(size_t)smp_bucket * W.paths + mi] = i;
 }
@@ -1281,22 +1300,22 @@ __global__ __launch_bounds__(kBlockSh) void k_nee_compact(WFState W, int b) {
     const int n = *cnt(W, b, kShadowQ);
     const int base = (int)(blockIdx.x * kBlockSh * kCompactPer);
     if (base >= n) return;  // block-uniform
-    __shared__ int lds[kShadeBuckets * (kWavesSh + 1)];
+    __shared__ int lds[kNeeBuckets * (kWavesSh + 1)];
     const int j0 = base + (int)threadIdx.x * kCompactPer;
     const bool cx = wf_cancelled(W);  // a cancelled wave compacts nothing but joins the barriers
     int v[kCompactPer];
-    int c[kShadeBuckets] = {};
+    int c[kNeeBuckets] = {};
 #pragma unroll
     for (int k = 0; k < kCompactPer; ++k) {
         v[k] = j0 + k < n && !cx ? W.vis[j0 + k] : -1;
 #pragma unroll
-        for (int q = 0; q < kShadeBuckets; ++q) c[q] += (v[k] >= 0 && (v[k] >> kItemBits) == q) ? 1 : 0;
+        for (int q = 0; q < kNeeBuckets; ++q) c[q] += (v[k] >= 0 && (v[k] >> kItemBits) == q) ? 1 : 0;
     }
     // block-exclusive prefix of every bucket's count: wave scan, then the wave totals in LDS
     const int lane = lane_id(), wave = threadIdx.x >> 6;
-    int incl[kShadeBuckets];
+    int incl[kNeeBuckets];
 #pragma unroll
-    for (int q = 0; q < kShadeBuckets; ++q) {
+    for (int q = 0; q < kNeeBuckets; ++q) {
         int x = c[q];
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1307,7 +1326,7 @@ __global__ __launch_bounds__(kBlockSh) void k_nee_compact(WFState W, int b) {
         if (lane == 63) lds[q * kWavesSh + wave] = x;
     }
     __syncthreads();
-    if ((int)threadIdx.x < kShadeBuckets) {
+    if ((int)threadIdx.x < kNeeBuckets) {
         const int q = threadIdx.x;
         int tot = 0;
         for (int w = 0; w < kWavesSh; ++w) {
@@ -1315,23 +1334,23 @@ __global__ __launch_bounds__(kBlockSh) void k_nee_compact(WFState W, int b) {
             lds[q * kWavesSh + w] = tot;
             tot += t;
         }
-        lds[kShadeBuckets * kWavesSh + q] = tot > 0 ? atomicAdd(cnt(W, b, kNee0 + q), tot) : 0;
+        lds[kNeeBuckets * kWavesSh + q] = tot > 0 ? atomicAdd(cnt(W, b, kNee0 + q), tot) : 0;
     }
     __syncthreads();
-    int off[kShadeBuckets];
+    int off[kNeeBuckets];
 #pragma unroll
-    for (int q = 0; q < kShadeBuckets; ++q)
-        off[q] = lds[kShadeBuckets * kWavesSh + q] + lds[q * kWavesSh + wave] + incl[q] - c[q];
+    for (int q = 0; q < kNeeBuckets; ++q)
+        off[q] = lds[kNeeBuckets * kWavesSh + q] + lds[q * kWavesSh + wave] + incl[q] - c[q];
 #pragma unroll
     for (int k = 0; k < kCompactPer; ++k) {
         if (v[k] < 0) continue;
         const int q = v[k] >> kItemBits;
         int slot = off[0];
 #pragma unroll
-        for (int r = 1; r < kShadeBuckets; ++r) slot = q == r ? off[r] : slot;
+        for (int r = 1; r < kNeeBuckets; ++r) slot = q == r ? off[r] : slot;
 #pragma unroll
-        for (int r = 0; r < kShadeBuckets; ++r) off[r] += q == r ? 1 : 0;
-        W.nq[(size_t)q * W.paths + slot] = v[k] & ((1 << kItemBits) - 1);
+        for (int r = 0; r < kNeeBuckets; ++r) off[r] += q == r ? 1 : 0;
+        W.nq[nee_index(W, q, slot)] = v[k] & ((1 << kItemBits) - 1);
     }
 }
 
@@ -1348,6 +1367,17 @@ __device__ __forceinline__ int bucket_entry(const WFState& W, const int* q, int 
 __device__ __forceinline__ int bucket_total(const WFState& W, int b, int c0) {
     return *cnt(W, b, c0) + *cnt(W, b, c0 + 1) + *cnt(W, b, c0 + 2);
 }
+// The NEE queue: bucket_entry's three regions, then the kNeeCross items from the back of region 2
+__device__ __forceinline__ int nee_entry(const WFState& W, int b, int idx) {
+    if (!PT_NEE_CROSS) return bucket_entry(W, W.nq, b, kNee0, idx);
+    const int n012 = bucket_total(W, b, kNee0);
+    if (idx < n012) return bucket_entry(W, W.nq, b, kNee0, idx);
+    const int k = idx - n012;
+    return k < *cnt(W, b, kNee0 + kNeeCross) ? W.nq[nee_index(W, kNeeCross, k)] : -1;
+}
+__device__ __forceinline__ int nee_total(const WFState& W, int b) {
+    return bucket_total(W, b, kNee0) + (PT_NEE_CROSS ? *cnt(W, b, kNee0 + kNeeCross) : 0);
+}
 
 // NEE of a Default / Layered bounce over the items whose light is visible (devicePrograms.cu:
 // 446-472).  The stochastic GlossyDiffuse eval dominates (≈10^4 instructions per call, DESIGN.md
@@ -1358,10 +1388,10 @@ __device__ __forceinline__ int bucket_total(const WFState& W, int b, int c0) {
 template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene S, DevLaunch L, WFState W, int b) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && L.counters)
-        atomicAdd(&L.counters[15], (unsigned long long)bucket_total(W, b, kNee0));
-    if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kNee0)) return;  // block-uniform
+        atomicAdd(&L.counters[15], (unsigned long long)nee_total(W, b));
+    if ((int)(blockIdx.x * kBlockShB) >= nee_total(W, b)) return;  // block-uniform
     if (wf_cancelled(W)) return;  // no barrier below
-    const int j = bucket_entry(W, W.nq, b, kNee0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
+    const int j = nee_entry(W, b, (int)(blockIdx.x * kBlockShB + threadIdx.x));
     if (j < 0) return;
     const float4 hv = W.hit[j], c = W.ray_d[b & 1][j];
     const int path = __float_as_int(hv.x);
@@ -1385,6 +1415,24 @@ __global__ __launch_bounds__(kBlockShB, PT_SHB_WAVES) void k_shade_nee(DevScene 
         d2 = dd.x * dd.x + dd.y * dd.y + dd.z * dd.z;
     }
     const float cosl = abs_dot(lds, mk(0.0f, 0.0f, 1.0f));
+#if PT_NEE_PROBE
+    // probe build only (tools/nee_probe.py): waves of the layered walk, those of them on its run-time
+    // path (some lane has the light across the shading plane) and those with both top kinds
+    if (L.counters) {
+        const bool lay = MODE == kModeLayered || !(aux & 1);
+        const unsigned long long any = __builtin_amdgcn_ballot_w64(lay);
+        const unsigned long long cross = __builtin_amdgcn_ballot_w64(lay && !same_hemisphere(sf.wo, lds));
+        const unsigned long long spec = __builtin_amdgcn_ballot_w64(lay && sqr(sf.roughness) < 1e-3f);
+        const unsigned long long act = __builtin_amdgcn_ballot_w64(true);
+        if (lane_id() == __ffsll((long long)act) - 1 && any) {
+            atomicAdd(&L.counters[21], 1ull);
+            if (cross) atomicAdd(&L.counters[20], 1ull);
+            if (spec && spec != any) atomicAdd(&L.counters[22], 1ull);
+            atomicAdd(&L.counters[23], (unsigned long long)__popcll(cross));
+            atomicAdd(&L.counters[24], (unsigned long long)__popcll(any));
+        }
+    }
+#endif
     f3 f = bsdf_f<MODE, true>(seed, sf.albedo, sf.roughness, aux & 1, sf.wo, lds);
     f3 spectrum = f * cosl;
     const float4 bv = W.beta[path];
