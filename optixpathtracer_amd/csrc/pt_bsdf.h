@@ -726,9 +726,24 @@ __device__ __forceinline__ f3 layered_f(uint32_t& seed, f3 albedo, float roughne
 // side takes the compile-time walk, any other wave the run-time one (same_hemisphere is invariant
 // under the walk's flip of both directions).
 #ifndef PT_LAYERED_SPLIT
-#define PT_LAYERED_SPLIT 1
+#define PT_LAYERED_SPLIT 3
 #endif
 __device__ __forceinline__ f3 layered_f_split(uint32_t& seed, f3 albedo, float roughness, f3 wo, f3 wi) {
+    if (PT_LAYERED_SPLIT >= 4) {  // as 3, a wave with both top kinds runs both compiled walks, masked
+        if (__builtin_amdgcn_ballot_w64(!same_hemisphere(wo, wi)) == 0) {
+            if (sqr(roughness) < 1e-3f) return layered_f_t<1, 2>(seed, albedo, roughness, wo, wi);
+            return layered_f_t<1, 1>(seed, albedo, roughness, wo, wi);
+        }
+        return layered_f_t<0>(seed, albedo, roughness, wo, wi);
+    }
+    if (PT_LAYERED_SPLIT >= 3) {  // two specialised walks and the run-time one: no third copy
+        if (__builtin_amdgcn_ballot_w64(!same_hemisphere(wo, wi)) == 0) {
+            const bool spec = sqr(roughness) < 1e-3f;
+            if (__builtin_amdgcn_ballot_w64(spec) == 0) return layered_f_t<1, 1>(seed, albedo, roughness, wo, wi);
+            if (__builtin_amdgcn_ballot_w64(!spec) == 0) return layered_f_t<1, 2>(seed, albedo, roughness, wo, wi);
+        }
+        return layered_f_t<0>(seed, albedo, roughness, wo, wi);
+    }
     if (PT_LAYERED_SPLIT && __builtin_amdgcn_ballot_w64(!same_hemisphere(wo, wi)) == 0) {
         if (PT_LAYERED_SPLIT >= 2) {  // the top interface's kind, wave-uniform in all but a bucket's last wave
             const bool spec = sqr(roughness) < 1e-3f;
@@ -740,8 +755,14 @@ __device__ __forceinline__ f3 layered_f_split(uint32_t& seed, f3 albedo, float r
     return layered_f_t<0>(seed, albedo, roughness, wo, wi);
 }
 
-PT_LAYERED_FN_S bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+// TOPK = 1 / 2: the caller guarantees a rough / smooth top interface for every lane of the wave
+// (layered_sample_split), so the dielectric helpers' alpha tests fold
+template <int TOPK = 0>
+PT_LAYERED_FN_S bool layered_sample_t(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
     // GlossyDiffuse.h:372-524
+    const float alpha = sqr(roughness);
+    if (TOPK == 1) __builtin_assume(!(alpha < 1e-3f));
+    if (TOPK == 2) __builtin_assume(alpha < 1e-3f);
     const int mode = kRadiance;
     const float thickness = 0.01f;
     bool flipWi = false;
@@ -804,19 +825,41 @@ PT_LAYERED_FN_S bool layered_sample(uint32_t& seed, f3 albedo, float roughness, 
     }
     return false;
 }
+__device__ __forceinline__ bool layered_sample(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+    return layered_sample_t<0>(seed, albedo, roughness, wo, out);
+}
+// The sample kernel's entry (PT_LAYERED_SAMPLE_SPLIT): a wave whose lanes share the top
+// interface's kind (all but a bucket's last wave) takes that kind's compiled walk
+#ifndef PT_LAYERED_SAMPLE_SPLIT
+#define PT_LAYERED_SAMPLE_SPLIT 0
+#endif
+__device__ __forceinline__ bool layered_sample_split(uint32_t& seed, f3 albedo, float roughness, f3 wo, BSample& out) {
+    if (PT_LAYERED_SAMPLE_SPLIT >= 2) {  // the two compiled walks only: a mixed wave runs both, masked
+        if (sqr(roughness) < 1e-3f) return layered_sample_t<2>(seed, albedo, roughness, wo, out);
+        return layered_sample_t<1>(seed, albedo, roughness, wo, out);
+    }
+    if (PT_LAYERED_SAMPLE_SPLIT) {
+        const bool spec = sqr(roughness) < 1e-3f;
+        if (__builtin_amdgcn_ballot_w64(spec) == 0) return layered_sample_t<1>(seed, albedo, roughness, wo, out);
+        if (__builtin_amdgcn_ballot_w64(!spec) == 0) return layered_sample_t<2>(seed, albedo, roughness, wo, out);
+    }
+    return layered_sample_t<0>(seed, albedo, roughness, wo, out);
+}
 
 // ---- material dispatch: devicePrograms.cu:303-341 (+ commented alternatives) ---------------
 enum MaterialMode { kModeDefault = 0, kModeLambert = 1, kModeConductor = 2, kModeDielectric = 3, kModeLayered = 4 };
 
-template <int MODE>
+// SPLIT: the layered sample through layered_sample_split (the bucketed sample kernel)
+template <int MODE, bool SPLIT = false>
 __device__ __forceinline__ bool bsdf_sample(uint32_t& seed, f3 albedo, float roughness, bool conductor, f3 wo,
                                             BSample& bs) {
     if (MODE == kModeLambert) return lambert_sample(seed, albedo, true, bs);
     if (MODE == kModeConductor) return conductor_sample(seed, albedo, roughness, wo, bs);
     if (MODE == kModeDielectric) return dielectric_sample(seed, roughness, wo, bs, kRadiance, true, true);
-    if (MODE == kModeLayered) return layered_sample(seed, albedo, roughness, wo, bs);
+    if (MODE == kModeLayered)
+        return SPLIT ? layered_sample_split(seed, albedo, roughness, wo, bs) : layered_sample(seed, albedo, roughness, wo, bs);
     if (conductor) return conductor_sample(seed, albedo, roughness, wo, bs);
-    return layered_sample(seed, albedo, roughness, wo, bs);
+    return SPLIT ? layered_sample_split(seed, albedo, roughness, wo, bs) : layered_sample(seed, albedo, roughness, wo, bs);
 }
 // SPLIT: the layered eval through layered_f_split (the bucketed NEE kernel)
 template <int MODE, bool SPLIT = false>

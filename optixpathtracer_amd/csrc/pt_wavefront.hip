@@ -1491,7 +1491,7 @@ __global__ __launch_bounds__(kBlockShB, PT_SMP_WAVES) void k_shade_smp(DevScene 
         uint32_t seed = __float_as_uint(bv.w);
         f3 beta = mk(bv.x, bv.y, bv.z);
         BSample bs;
-        if (bsdf_sample<MODE>(seed, sf.albedo, sf.roughness, W.aux[path] & 1, sf.wo, bs)) {
+        if (bsdf_sample<MODE, true>(seed, sf.albedo, sf.roughness, W.aux[path] & 1, sf.wo, bs)) {
             emit_next = continue_path(sf, bs, beta, o, d, b + 1, L.max_bounces);
             W.beta[path] = make_float4(beta.x, beta.y, beta.z, __uint_as_float(seed));
         }

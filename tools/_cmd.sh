@@ -1,5 +1,4 @@
-#!/bin/bash
 set -o pipefail
-mkdir -p gpurun_out
-PTAMD_LIB=optixpathtracer_amd/_variants/lib_tail.so timeout -k 10 300 python3 tools/perf_probe.py --scene sphere_box_diffuse --fpl 128 --spp 128 --repeat 1 --modes 1,3 > gpurun_out/r05zz_tail_final.log 2>&1 || exit 1
-grep -c TAIL gpurun_out/r05zz_tail_final.log
+mkdir -p gpurun_out/r06u
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r06u/gputest.log 2>&1 || { tail -30 gpurun_out/r06u/gputest.log; exit 1; }
+tail -1 gpurun_out/r06u/gputest.log
