@@ -192,23 +192,49 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
 constexpr int kShadeBuckets = 3;
 // PT_NEE_CROSS (round 6): the NEE items have one more bucket, kNeeCross: layered items whose light
 // lies across the shading plane from the viewer, so that every other layered NEE wave runs the
-// walk's compile-time path (layered_f_split).  Its queue region is bucket 2's, filled from the back
-// (nee_index).  Without it 70 % of Sponza-class's and 45 % of Layered's walk waves held such a
-// lane (4.2 / 1.6 % of the lanes, tools/nee_probe.py) and ran the run-time walk.
+// walk's compile-time path (layered_f_split).  Without it 70 % of Sponza-class's and 45 % of
+// Layered's walk waves held such a lane (4.2 / 1.6 % of the lanes, tools/nee_probe.py) and ran the
+// run-time walk.
+// PT_NEE_DARK (> 0, needs PT_NEE_CROSS): layered items whose albedo's largest channel is below it
+// take buckets of their own beside the smooth and rough ones (kNeeDark0 + 0 / 1): the walk's
+// Russian roulette ends dark walks early, so a wave of them no longer waits for a bright lane.
+// Buckets 0-2 fill regions 0-2 of W.nq from the front; the others fill a region from the back
+// (nee_index), since a bounce queues at most W.paths NEE items in all.
 #ifndef PT_NEE_CROSS
 #define PT_NEE_CROSS 1
 #endif
-constexpr int kNeeBuckets = kShadeBuckets + (PT_NEE_CROSS ? 1 : 0);
+#ifndef PT_NEE_DARK
+#define PT_NEE_DARK 0.5f
+#endif
+// PT_SMP_DARK (> 0): the same split of the BSDF-sample items (the sample walk's roulette alike):
+// kSmpDark0 + 0 / 1 beside buckets 1 / 2, from the back of regions 1 / 2 of W.sq
+#ifndef PT_SMP_DARK
+#define PT_SMP_DARK 0.0f
+#endif
+constexpr bool kSmpDark = PT_SMP_DARK > 0.0f;
+constexpr int kSmpBuckets = kShadeBuckets + (kSmpDark ? 2 : 0);
+constexpr int kSmpDark0 = kShadeBuckets;
+constexpr bool kNeeDark = PT_NEE_CROSS && PT_NEE_DARK > 0.0f;
+constexpr int kNeeBuckets = kShadeBuckets + (PT_NEE_CROSS ? 1 : 0) + (kNeeDark ? 2 : 0);
 constexpr int kNeeCross = kShadeBuckets;
-constexpr int kCnt = 5 + kNeeBuckets + kShadeBuckets;
+constexpr int kNeeDark0 = kShadeBuckets + 1;
+constexpr int kCnt = 5 + kNeeBuckets + kSmpBuckets;
 constexpr int kCntStride = 32;  // ints per counter = 128 B
 // kPool*: the run-time ray pools of k_trace_pair, k_extend and k_shadow_vis (RayPool)
-enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kNeeBuckets, kPool = 2 + kNeeBuckets + kShadeBuckets, kPoolExt, kPoolSh };
+enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kNeeBuckets, kPool = 2 + kNeeBuckets + kSmpBuckets, kPoolExt, kPoolSh };
 __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
-// Slot `slot` of NEE bucket q in W.nq: region q, or for kNeeCross the back of region 2 (a bounce
-// queues at most W.paths NEE items in all, so the two ends never meet)
+// Slot `slot` of NEE bucket q in W.nq: region q from the front for q < 3; from the back, region 0
+// for kNeeCross (region 2 without the dark buckets) and regions 1 / 2 for the dark buckets
 __device__ __forceinline__ size_t nee_index(const WFState& W, int q, int slot) {
-    return q < kShadeBuckets ? (size_t)q * W.paths + slot : (size_t)kShadeBuckets * W.paths - 1 - slot;
+    if (q < kShadeBuckets) return (size_t)q * W.paths + slot;
+    const int region = q == kNeeCross ? (kNeeDark ? 0 : 2) : q - kNeeDark0 + 1;
+    return (size_t)(region + 1) * W.paths - 1 - slot;
+}
+// Slot `slot` of sample bucket q in W.sq: region q from the front, the dark buckets from the back
+// of regions 1 / 2
+__device__ __forceinline__ size_t smp_index(const WFState& W, int q, int slot) {
+    if (q < kShadeBuckets) return (size_t)q * W.paths + slot;
+    return (size_t)(q - kSmpDark0 + 2) * W.paths - 1 - slot;
 }
 // Path throughput | seed.  W.beta in path order (the phases of a bounce read it by path), except
 // in the Lambert mode: in queue order next to the ray, ping-pong like ray_o / ray_d (queue b
@@ -1195,7 +1221,7 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
     const int n = *cnt(W, b, kQueue);
     const float4* rd = W.ray_d[b & 1];
     __shared__ int lds_sh[kWavesShA + 1];
-    __shared__ int lds_nee[kNeeBuckets * (kWavesShA + 1)], lds_smp[kShadeBuckets * (kWavesShA + 1)];
+    __shared__ int lds_nee[kNeeBuckets * (kWavesShA + 1)], lds_smp[kSmpBuckets * (kWavesShA + 1)];
     if ((int)(blockIdx.x * kBlockShA) >= n) return;  // block-uniform
     const int i = (int)(blockIdx.x * kBlockShA + threadIdx.x);
     bool emit = false;
@@ -1224,14 +1250,23 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
             W.aux[path] = (li << 1) | (conductor ? 1 : 0);
             const int bk = shade_bucket<MODE>(conductor, sf.roughness);
             // the last bounce's sampled direction is never traced (SamplePath :646): no sample item
-            if (b + 1 < L.max_bounces) smp_bucket = bk;
+            if (b + 1 < L.max_bounces) {
+                smp_bucket = bk;
+                if (kSmpDark && (MODE == kModeLayered || !conductor) &&
+                    fmaxf(fmaxf(sf.albedo.x, sf.albedo.y), sf.albedo.z) < PT_SMP_DARK)
+                    smp_bucket = kSmpDark0 + bk - 1;
+            }
             if (P > 0.0f) {
                 const DevLight lt = L.lights[li];
                 f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
                 const f3 ln = normalize(ldir);  // k_shade_nee's light direction, the same bits
                 int nb = bk;
-                if (PT_NEE_CROSS && (MODE == kModeLayered || !conductor) && !same_hemisphere(sf.wo, to_local(sf.fr, ln)))
-                    nb = kNeeCross;
+                if (MODE == kModeLayered || !conductor) {
+                    if (PT_NEE_CROSS && !same_hemisphere(sf.wo, to_local(sf.fr, ln)))
+                        nb = kNeeCross;
+                    else if (kNeeDark && fmaxf(fmaxf(sf.albedo.x, sf.albedo.y), sf.albedo.z) < PT_NEE_DARK)
+                        nb = kNeeDark0 + bk - 1;
+                }
                 if (vis0) {
                     if (W.vis[vis0_index(L, path, li)]) nee_bucket = nb;
                 } else {
@@ -1251,8 +1286,8 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
     }
     const int ni = block_append_k<kWavesShA, kNeeBuckets>(cnt(W, b, kNee0), nee_bucket, lds_nee);
     if (nee_bucket >= 0) W.nq[nee_index(W, nee_bucket, ni)] = i;
-    const int mi = block_append_k<kWavesShA, kShadeBuckets>(cnt(W, b, kSmp0), smp_bucket, lds_smp);
-    if (smp_bucket >= 0) W.sq[(size_t)smp_bucket * W.paths + mi] = i;
+    const int mi = block_append_k<kWavesShA, kSmpBuckets>(cnt(W, b, kSmp0), smp_bucket, lds_smp);
+    if (smp_bucket >= 0) W.sq[smp_index(W, smp_bucket, mi)] = i;
 }
 
 // Any-hit visibility of the shadow queue of bounce b.  table = 1: the bounce-0 (pixel, light)
@@ -1354,29 +1389,40 @@ __global__ __launch_bounds__(kBlockSh) void k_nee_compact(WFState W, int b) {
     }
 }
 
-// Entry idx of a bucketed queue (region k: q[k * paths ...], length *cnt(W, b, c0 + k)), or -1
-// past the total.  Regions are taken in bucket order, so all but two waves hold one bucket.
-__device__ __forceinline__ int bucket_entry(const WFState& W, const int* q, int b, int c0, int idx) {
-    const int n0 = *cnt(W, b, c0), n1 = *cnt(W, b, c0 + 1), n2 = *cnt(W, b, c0 + 2);
-    static_assert(kShadeBuckets == 3, "bucket_entry walks three regions");
-    if (idx < n0) return q[idx];
-    if (idx < n0 + n1) return q[(size_t)W.paths + (idx - n0)];
-    if (idx < n0 + n1 + n2) return q[2 * (size_t)W.paths + (idx - n0 - n1)];
+// Entry idx of the NEE / sample queue (bucket q: slots nee_index / smp_index, length
+// *cnt(W, b, c0 + q)), or -1 past the total.  Buckets are taken in order, so all but a few waves
+// hold one bucket.
+__device__ __forceinline__ int nee_entry(const WFState& W, int b, int idx) {
+    int base = 0;
+#pragma unroll
+    for (int q = 0; q < kNeeBuckets; ++q) {
+        const int n = *cnt(W, b, kNee0 + q);
+        if (idx < base + n) return W.nq[nee_index(W, q, idx - base)];
+        base += n;
+    }
     return -1;
 }
-__device__ __forceinline__ int bucket_total(const WFState& W, int b, int c0) {
-    return *cnt(W, b, c0) + *cnt(W, b, c0 + 1) + *cnt(W, b, c0 + 2);
+__device__ __forceinline__ int smp_entry(const WFState& W, int b, int idx) {
+    int base = 0;
+#pragma unroll
+    for (int q = 0; q < kSmpBuckets; ++q) {
+        const int n = *cnt(W, b, kSmp0 + q);
+        if (idx < base + n) return W.sq[smp_index(W, q, idx - base)];
+        base += n;
+    }
+    return -1;
 }
-// The NEE queue: bucket_entry's three regions, then the kNeeCross items from the back of region 2
-__device__ __forceinline__ int nee_entry(const WFState& W, int b, int idx) {
-    if (!PT_NEE_CROSS) return bucket_entry(W, W.nq, b, kNee0, idx);
-    const int n012 = bucket_total(W, b, kNee0);
-    if (idx < n012) return bucket_entry(W, W.nq, b, kNee0, idx);
-    const int k = idx - n012;
-    return k < *cnt(W, b, kNee0 + kNeeCross) ? W.nq[nee_index(W, kNeeCross, k)] : -1;
+__device__ __forceinline__ int smp_total(const WFState& W, int b) {
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < kSmpBuckets; ++q) n += *cnt(W, b, kSmp0 + q);
+    return n;
 }
 __device__ __forceinline__ int nee_total(const WFState& W, int b) {
-    return bucket_total(W, b, kNee0) + (PT_NEE_CROSS ? *cnt(W, b, kNee0 + kNeeCross) : 0);
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < kNeeBuckets; ++q) n += *cnt(W, b, kNee0 + q);
+    return n;
 }
 
 // NEE of a Default / Layered bounce over the items whose light is visible (devicePrograms.cu:
@@ -1475,8 +1521,8 @@ template <int MODE, bool TEX>
 __global__ __launch_bounds__(kBlockShB, PT_SMP_WAVES) void k_shade_smp(DevScene S, DevLaunch L, WFState W, int b) {
     constexpr int kW = kBlockShB / 64;
     __shared__ int lds_q[kW + 1];
-    if ((int)(blockIdx.x * kBlockShB) >= bucket_total(W, b, kSmp0)) return;  // block-uniform
-    const int j = bucket_entry(W, W.sq, b, kSmp0, (int)(blockIdx.x * kBlockShB + threadIdx.x));
+    if ((int)(blockIdx.x * kBlockShB) >= smp_total(W, b)) return;  // block-uniform
+    const int j = smp_entry(W, b, (int)(blockIdx.x * kBlockShB + threadIdx.x));
     bool emit_next = false;
     f3 o, d;
     int path = 0;
