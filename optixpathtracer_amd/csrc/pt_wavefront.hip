@@ -190,23 +190,33 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long* counters, c
 // Default / Layered shading items are queued per bucket (shade_bucket): kNeeBuckets NEE and
 // kShadeBuckets BSDF-sample counters follow the two queue counters.
 constexpr int kShadeBuckets = 3;
-// PT_NEE_CROSS (round 6): the NEE items have one more bucket, kNeeCross: layered items whose light
-// lies across the shading plane from the viewer, so that every other layered NEE wave runs the
-// walk's compile-time path (layered_f_split).  Without it 70 % of Sponza-class's and 45 % of
-// Layered's walk waves held such a lane (4.2 / 1.6 % of the lanes, tools/nee_probe.py) and ran the
-// run-time walk.
-// PT_NEE_DARK (> 0, needs PT_NEE_CROSS): layered items whose albedo's largest channel is below it
-// take buckets of their own beside the smooth and rough ones (kNeeDark0 + 0 / 1): the walk's
-// Russian roulette ends dark walks early, so a wave of them no longer waits for a bright lane.
-// Buckets 0-2 fill regions 0-2 of W.nq from the front; the others fill a region from the back
-// (nee_index), since a bounce queues at most W.paths NEE items in all.
+// NEE buckets (round 6): 0 = conductor; 1 = kNeeCross, layered items whose light lies across the
+// shading plane from the viewer (PT_NEE_CROSS), so that every other layered NEE wave runs the
+// walk's compile-time path (layered_f_split; without it 70 % of Sponza-class's and 45 % of
+// Layered's walk waves held such a lane, 4.2 / 1.6 % of the lanes, tools/nee_probe.py); then per
+// albedo class k (kNeeClasses) the layered items with a smooth (2 + 2k) and a rough (3 + 2k) top.
+// The walk's Russian roulette ends walks over a dark bottom layer early, so a wave that mixes
+// them with bright ones runs as long as its brightest lane: the class of an item is the largest
+// channel of its albedo against PT_NEE_MID (classes >= 3) and PT_NEE_DARK (classes >= 2).
+// Bucket q fills region q / 2 of W.nq from the front (q even) or the back (q odd): a bounce
+// queues at most W.paths NEE items in all, so the two ends of a region never meet.
 #ifndef PT_NEE_CROSS
 #define PT_NEE_CROSS 1
+#endif
+#ifndef PT_NEE_CLASSES
+#define PT_NEE_CLASSES 2
 #endif
 #ifndef PT_NEE_DARK
 #define PT_NEE_DARK 0.5f
 #endif
-// PT_SMP_DARK (> 0): the same split of the BSDF-sample items (the sample walk's roulette alike):
+#ifndef PT_NEE_MID
+#define PT_NEE_MID 0.7f
+#endif
+constexpr int kNeeClasses = PT_NEE_CLASSES;
+constexpr int kNeeBuckets = 2 + 2 * kNeeClasses;
+constexpr int kNeeRegions = kNeeBuckets / 2;
+constexpr int kNeeCross = 1;
+// PT_SMP_DARK (> 0): a dark class of the BSDF-sample items, as PT_NEE_DARK (not kept):
 // kSmpDark0 + 0 / 1 beside buckets 1 / 2, from the back of regions 1 / 2 of W.sq
 #ifndef PT_SMP_DARK
 #define PT_SMP_DARK 0.0f
@@ -214,21 +224,23 @@ constexpr int kShadeBuckets = 3;
 constexpr bool kSmpDark = PT_SMP_DARK > 0.0f;
 constexpr int kSmpBuckets = kShadeBuckets + (kSmpDark ? 2 : 0);
 constexpr int kSmpDark0 = kShadeBuckets;
-constexpr bool kNeeDark = PT_NEE_CROSS && PT_NEE_DARK > 0.0f;
-constexpr int kNeeBuckets = kShadeBuckets + (PT_NEE_CROSS ? 1 : 0) + (kNeeDark ? 2 : 0);
-constexpr int kNeeCross = kShadeBuckets;
-constexpr int kNeeDark0 = kShadeBuckets + 1;
 constexpr int kCnt = 5 + kNeeBuckets + kSmpBuckets;
 constexpr int kCntStride = 32;  // ints per counter = 128 B
 // kPool*: the run-time ray pools of k_trace_pair, k_extend and k_shadow_vis (RayPool)
 enum { kQueue = 0, kShadowQ = 1, kNee0 = 2, kSmp0 = 2 + kNeeBuckets, kPool = 2 + kNeeBuckets + kSmpBuckets, kPoolExt, kPoolSh };
 __device__ __forceinline__ int* cnt(const WFState& W, int b, int k) { return W.count + (kCnt * b + k) * kCntStride; }
-// Slot `slot` of NEE bucket q in W.nq: region q from the front for q < 3; from the back, region 0
-// for kNeeCross (region 2 without the dark buckets) and regions 1 / 2 for the dark buckets
+// Slot `slot` of NEE bucket q in W.nq
 __device__ __forceinline__ size_t nee_index(const WFState& W, int q, int slot) {
-    if (q < kShadeBuckets) return (size_t)q * W.paths + slot;
-    const int region = q == kNeeCross ? (kNeeDark ? 0 : 2) : q - kNeeDark0 + 1;
-    return (size_t)(region + 1) * W.paths - 1 - slot;
+    const size_t r = (size_t)(q >> 1) * W.paths;
+    return (q & 1) ? r + W.paths - 1 - slot : r + slot;
+}
+// NEE bucket of a layered item (sample bucket bk 1 / 2: smooth / rough top) from its albedo
+__device__ __forceinline__ int nee_layered_bucket(int bk, f3 albedo) {
+    const float m = fmaxf(fmaxf(albedo.x, albedo.y), albedo.z);
+    int cls = 0;
+    if (kNeeClasses >= 3 && m < PT_NEE_MID) cls = 1;
+    if (kNeeClasses >= 2 && m < PT_NEE_DARK) cls = kNeeClasses - 1;
+    return 2 + 2 * cls + (bk - 1);
 }
 // Slot `slot` of sample bucket q in W.sq: region q from the front, the dark buckets from the back
 // of regions 1 / 2
@@ -1260,13 +1272,10 @@ __global__ __launch_bounds__(kBlockShA) void k_shade_a(DevScene S, DevLaunch L, 
                 const DevLight lt = L.lights[li];
                 f3 ldir = mk(lt.px, lt.py, lt.pz) - sf.pos;
                 const f3 ln = normalize(ldir);  // k_shade_nee's light direction, the same bits
-                int nb = bk;
-                if (MODE == kModeLayered || !conductor) {
-                    if (PT_NEE_CROSS && !same_hemisphere(sf.wo, to_local(sf.fr, ln)))
-                        nb = kNeeCross;
-                    else if (kNeeDark && fmaxf(fmaxf(sf.albedo.x, sf.albedo.y), sf.albedo.z) < PT_NEE_DARK)
-                        nb = kNeeDark0 + bk - 1;
-                }
+                int nb = 0;  // conductor
+                if (MODE == kModeLayered || !conductor)
+                    nb = PT_NEE_CROSS && !same_hemisphere(sf.wo, to_local(sf.fr, ln)) ? kNeeCross
+                                                                                     : nee_layered_bucket(bk, sf.albedo);
                 if (vis0) {
                     if (W.vis[vis0_index(L, path, li)]) nee_bucket = nb;
                 } else {
@@ -1704,7 +1713,7 @@ hipError_t accum_f64_to_f32(const double* sum64, float* sum32, size_t n, hipStre
 size_t wavefront_bytes(int paths, int max_bounces) {
     size_t P = (size_t)paths;
     return P * sizeof(float4) * (4 /*rays x2 queues*/ + 1 /*hit*/ + 3 /*beta x2, L*/ + 3 /*shadow*/) +
-           P * (2 + 2 * kShadeBuckets) * sizeof(int) + count_bytes(max_bounces);
+           P * (2 + kNeeRegions + kShadeBuckets) * sizeof(int) + count_bytes(max_bounces);
 }
 
 hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
@@ -1726,7 +1735,7 @@ hipError_t wavefront_alloc(WFState& W, int paths, int max_bounces) {
     al((void**)&W.sh_c, P * sizeof(float4));
     al((void**)&W.aux, P * sizeof(int));
     al((void**)&W.vis, P * sizeof(int));
-    al((void**)&W.nq, P * kShadeBuckets * sizeof(int));
+    al((void**)&W.nq, P * kNeeRegions * sizeof(int));
     al((void**)&W.sq, P * kShadeBuckets * sizeof(int));
     al((void**)&W.count, count_bytes(max_bounces));
     if (e != hipSuccess) {
