@@ -1,4 +1,4 @@
 set -o pipefail
-mkdir -p gpurun_out/r06z2
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r06z2/gputest.log 2>&1 || { tail -30 gpurun_out/r06z2/gputest.log; exit 1; }
-tail -1 gpurun_out/r06z2/gputest.log
+mkdir -p gpurun_out/r06z4
+tools/ab.sh "c256 p60 p80 p40 p60b" 4 --scene sphere_box_diffuse --fpl 128 --spp 256 --repeat 2 > gpurun_out/r06z4/ab_pool2_c2.log 2>&1 || exit 1
+python3 tools/ab_summary.py gpurun_out/r06z4/ab_pool2_*.log
