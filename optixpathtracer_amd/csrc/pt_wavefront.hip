@@ -216,6 +216,7 @@ constexpr int kNeeClasses = PT_NEE_CLASSES;
 constexpr int kNeeBuckets = 2 + 2 * kNeeClasses;
 constexpr int kNeeRegions = kNeeBuckets / 2;
 constexpr int kNeeCross = 1;
+static_assert(kNeeBuckets <= 8, "a shadow ray's item code holds the NEE bucket in bits 28-30");
 // PT_SMP_DARK (> 0): a dark class of the BSDF-sample items, as PT_NEE_DARK (not kept):
 // kSmpDark0 + 0 / 1 beside buckets 1 / 2, from the back of regions 1 / 2 of W.sq
 #ifndef PT_SMP_DARK
@@ -424,7 +425,8 @@ __device__ __forceinline__ int block_append_k(int* counter0, int bucket, int* ld
 // path, so the NEE and sample kernels take them from per-bucket queue regions and their waves
 // hold one kind of item: 0 = conductor (Default mode's metallic coin, devicePrograms.cu:400),
 // 1 / 2 = the layered BSDF with a smooth / rough top interface (layered_f's topSpec: alpha =
-// roughness^2 < 1e-3, GlossyDiffuse.h).
+// roughness^2 < 1e-3, GlossyDiffuse.h).  These are the sample buckets; the NEE items split the
+// layered ones further (nee_layered_bucket, kNeeCross).
 template <int MODE>
 __device__ __forceinline__ int shade_bucket(bool conductor, float roughness) {
     if (MODE == kModeDefault && conductor) return 0;

@@ -1,4 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/r06z4
-tools/ab.sh "c256 p60 p80 p40 p60b" 4 --scene sphere_box_diffuse --fpl 128 --spp 256 --repeat 2 > gpurun_out/r06z4/ab_pool2_c2.log 2>&1 || exit 1
-python3 tools/ab_summary.py gpurun_out/r06z4/ab_pool2_*.log
+mkdir -p gpurun_out/r06z5
+for s in sponza_class:c5 sphere_box_conductor:c3 sphere_box_layered:4l; do
+  sc=${s%%:*}; tag=${s#*:}
+  tools/ab.sh "base w3 u1" 3 --scene $sc --fpl 128 --spp 256 --repeat 2 > gpurun_out/r06z5/ab_retune_$tag.log 2>&1 || exit 1
+done
+python3 tools/ab_summary.py gpurun_out/r06z5/ab_retune_*.log
