@@ -1,7 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/r06z6
+mkdir -p gpurun_out/r06z7
 for s in sponza_class:c5 sphere_box_conductor:c3 sphere_box_layered:4l; do
   sc=${s%%:*}; tag=${s#*:}
-  tools/ab.sh "base sha512 shb128 shb512" 3 --scene $sc --fpl 128 --spp 256 --repeat 2 > gpurun_out/r06z6/ab_blocks_$tag.log 2>&1 || exit 1
+  tools/ab.sh "first last" 3 --scene $sc --fpl 128 --spp 256 --repeat 2 > gpurun_out/r06z7/ab_order_$tag.log 2>&1 || exit 1
 done
-python3 tools/ab_summary.py gpurun_out/r06z6/ab_blocks_*.log
+python3 tools/ab_summary.py gpurun_out/r06z7/ab_order_*.log
